@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Headline benchmark: implicit Swift-Hohenberg Newton-Krylov time steps on a 4096^2 grid.
+
+Metric (BASELINE.json): "Newton-steps/sec + JVP SpMV HBM GB/s (% peak), 4096^2 grid, 1/2/4/8 GPU".
+A *step* is one implicit Crank-Nicolson time step = one full ``newton_krylov`` solve, exactly the
+loop body of the reference (sh_scipy_nk.py:56-61), on the config-4 workload: N = 4096,
+h = 0.625 (d = 0.625 N, SURVEY.md section 7 hard part 2), k = 0.2, r = 0.01, g = 1,
+U0 = default_rng(2020).standard_normal(N^2), scipy-default tolerances, FD (scipy-faithful) JVP.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+N > 1: the same 4096^2 grid is cut into N row slabs (strong scaling), RCCL halo + all-reduce.
+value = time steps per second of the whole job (max over ranks of the timed region).
+Rank 0 prints ONE JSON line.  The kernel roofline comes from HIP events recorded around every
+kernel on the solver's stream inside the timed region (nk_sh_kernel_profile).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "iterative-solvers-summer-2020_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Newton-steps/sec + JVP SpMV HBM GB/s (% peak), 4096^2 grid, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=4096, help="grid points per side")
+    ap.add_argument("--jvp", choices=["fd", "analytic"], default="fd")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, h, k, r, g, fevals_per_step):
+    """The reference's CPU path (scipy CSR L + scipy.optimize.newton_krylov, oracle/sh_oracle.py),
+    timed on a bounded sample: the FIRST Newton iteration of step 0 at the full grid size."""
+    import numpy as np
+    from scipy.optimize import NoConvergence, newton_krylov
+
+    from oracle import sh_oracle
+
+    L = sh_oracle.csr_L(n, h, r)
+    U0 = np.random.default_rng(2020).standard_normal(n * n)
+    cnt = [0]
+    f = sh_oracle.make_csr_residual(L, U0, k, g, cnt)
+    t0 = time.perf_counter()
+    try:
+        newton_krylov(f, U0, maxiter=1)
+    except NoConvergence:
+        pass
+    dt = time.perf_counter() - t0
+    s_per_feval = dt / max(cnt[0], 1)
+    step_s = s_per_feval * fevals_per_step
+    try:
+        import threadpoolctl
+        blas_threads = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
+    except Exception:
+        blas_threads = os.cpu_count() or 1
+    return {
+        "value": 1.0 / step_s,
+        "unit": "steps/s",
+        "cores": int(blas_threads),
+        "kind": "port",
+        "sample": (f"scipy CSR L ({L.nnz} nnz) + scipy.optimize.newton_krylov: first Newton "
+                   f"iteration of step 0 at {n}^2 ({cnt[0]} F evals incl. FD-JVPs, {dt:.1f} s, "
+                   f"{s_per_feval:.3f} s/F-eval incl. its LGMRES work); steps/s extrapolated with "
+                   f"the {fevals_per_step:.0f} F evals/step the GPU run needed (same algorithm). "
+                   f"csr_matvec and NumPy element-wise are single-threaded; OpenBLAS BLAS-1 uses "
+                   f"{blas_threads} threads; os.cpu_count()={os.cpu_count()}"),
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import nkhip
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    comm = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        comm = nkhip.RcclComm.from_torch_distributed()
+
+    n = args.n
+    h, k, r, g = 0.625, 0.2, 0.01, 1.0
+    row0, ny = nkhip.slab_rows(n, rank, world)
+    U_full = np.random.default_rng(2020).standard_normal((n, n))
+    U = torch.as_tensor(U_full[row0:row0 + ny].copy(), device="cuda")
+    del U_full
+    stream = torch.cuda.current_stream()
+    model = nkhip.SwiftHohenberg(N=n, d=h * n, k=k, r=r, g=g, jvp=args.jvp, profile=True,
+                                 comm=comm, ny_local=ny, stream=stream)
+    a, b = U, torch.empty_like(U)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        model.step(a, out=b)
+        a, b = b, a
+    model.reset_profile()
+    tot = {"nit": 0, "nfev": 0, "njvp": 0}
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.step(a, out=b)
+        for key in tot:
+            tot[key] += model.last_stats[key]
+        a, b = b, a
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = model.kernel_profile()
+    final_max = float(a.abs().max())
+
+    if rank == 0:
+        steps_per_s = args.steps / elapsed
+        # dominant kernel by time, and the JVP stencil the metric names
+        ker = {k_: v for k_, v in prof.items() if v["launches"] > 0 and v["ms"] > 0}
+        dom = max(ker, key=lambda k_: ker[k_]["ms"])
+
+        def roof(name):
+            v = ker[name]
+            gbs = v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9
+            return {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "traffic": None, "launches": v["launches"],
+                    "avg_us": round(1e3 * v["ms"] / v["launches"], 2),
+                    "alg_bytes_per_launch": v["alg_bytes"] / v["launches"]}
+
+        jvp_name = "sh_fdjvp" if args.jvp == "fd" else "sh_ajvp"
+        kernel_ms = sum(v["ms"] for v in ker.values())
+        out = {
+            "metric": METRIC,
+            "value": round(steps_per_s, 4),
+            "unit": "steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: U0 = numpy default_rng(2020).standard_normal(N^2)",
+            "config": {"workload": f"swift_hohenberg_cn_newton_krylov_{n}x{n}", "grid": [n, n],
+                       "h": h, "k": k, "r": r, "g": g, "jvp": args.jvp,
+                       "f_tol": "scipy default eps^(1/3) (max-norm)", "inner_m": 30,
+                       "outer_k": 10, "parallelism": f"row-slab x{world} (RCCL halo)"},
+            "newton_its_per_s": round(tot["nit"] / elapsed, 3),
+            "jvps_per_s": round(tot["njvp"] / elapsed, 2),
+            "per_step": {k_: v / args.steps for k_, v in tot.items()},
+            "roofline": roof(dom),
+            "jvp_roofline": roof(jvp_name) if jvp_name in ker else None,
+            "kernel_time_frac_of_wall": round(kernel_ms * 1e-3 / elapsed, 4),
+            "kernels": {k_: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                             "GB/s": round(v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)}
+                        for k_, v in ker.items()},
+            "state_max_abs": final_max,
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline == "auto":
+            fe = (tot["nfev"] + tot["njvp"]) / args.steps
+            out["cpu_baseline"] = cpu_baseline(n, h, k, r, g, fe)
+        print(json.dumps(out), flush=True)
+    model.close()
+    if comm is not None:
+        comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+/*
+ * nkhip.h -- C-ABI of the MI355X-native Newton-Krylov Swift-Hohenberg time-stepper.
+ *
+ * Every pointer argument named *_dev is a device (HBM) pointer to fp64 data; the caller owns
+ * all buffers.  `stream` is a hipStream_t passed as void* (NULL = the null stream).  No torch
+ * or Eigen types cross this boundary.  Grids are row-major, u[i*nx + j], i = y (row), j = x.
+ *
+ * Each entry point names the reference interface it replaces (file:line into the reference
+ * Shiakaron/Iterative-solvers-summer-2020, or into the third-party SciPy 1.15.3 it calls,
+ * prefixed scipy/).  The C++ twin's solver library is not vendored; its API was recovered from
+ * the symbols of cpp_work/NewtonKrylov_Implementation/Project1/Debug/newton_krylov.obj
+ *  and is cited as "NewtonKrylov lib".
+ *
+ * Return codes: NK_OK = 0; NK_NO_CONVERGENCE = 1 (scipy NoConvergence, _nonlin.py:247-249);
+ * NK_NONFINITE = 2 (ValueError 'Function returned non-finite results', _nonlin.py:1511-1512);
+ * NK_ZERO_STEP = 3 (ValueError 'Jacobian inversion yielded zero vector', _nonlin.py:213-216);
+ * < 0: argument (NK_EINVAL), HIP (NK_EHIP) or RCCL (NK_ECOMM) failure.
+ */
+#ifndef NKHIP_H
+#define NKHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NK_OK 0
+#define NK_NO_CONVERGENCE 1
+#define NK_NONFINITE 2
+#define NK_ZERO_STEP 3
+#define NK_EINVAL (-1)
+#define NK_EHIP (-2)
+#define NK_ECOMM (-3)
+#define NK_ENOMEM (-4)
+
+#define NK_JVP_FD 0       /* KrylovJacobian.matvec finite difference (scipy-faithful) */
+#define NK_JVP_ANALYTIC 1 /* exact J v = v/k - (L v + (2 g u - 3 u^2) v)/2 */
+
+/* Options of newton_krylov (scipy/optimize/_nonlin.py:1553-1603, nonlin_solve :122-268).
+ * NaN tolerances select the SciPy defaults: f_tol = eps^(1/3), the others +inf. */
+typedef struct nk_opts {
+  double f_tol, f_rtol, x_tol, x_rtol;
+  double rdiff;        /* <= 0: sqrt(eps) (_nonlin.py:1538-1539) */
+  int64_t maxiter;     /* <= 0: 100*(n+1) (_nonlin.py:188) */
+  int32_t inner_m;     /* lgmres inner_m, default 30 (lgmres.py:15) */
+  int32_t outer_k;     /* default 10 (_nonlin.py:1453) */
+  int32_t line_search; /* 1 = 'armijo' (default), 0 = None */
+  int32_t jvp_mode;    /* NK_JVP_FD (default) or NK_JVP_ANALYTIC */
+  int32_t verbose;     /* print "%d:  |F(x)| = %g; step %g" per Newton iteration */
+  int32_t profile;     /* record HIP events around every kernel (see nk_sh_kernel_profile) */
+} nk_opts;
+
+typedef struct nk_stats {
+  int64_t nit;         /* Newton iterations */
+  int64_t nfev;        /* residual evaluations (initial + line search) */
+  int64_t njvp;        /* Jacobian-vector products (one per Arnoldi step) */
+  int64_t n_arnoldi;   /* Arnoldi steps (== njvp) */
+  double fnorm_inf;    /* max|F(x)| at exit */
+  double fnorm_2;      /* ||F(x)||_2 at exit */
+  int32_t status;
+  int32_t pad_;
+} nk_stats;
+
+/* Per-kernel-class timings recorded with HIP events on the solver's stream. */
+typedef struct nk_kprof {
+  char name[32];
+  int64_t launches;
+  double total_ms;
+  double alg_bytes;    /* algorithmic HBM bytes summed over launches */
+} nk_kprof;
+
+typedef struct nk_comm nk_comm;
+typedef struct nk_sh nk_sh;
+
+const char* nk_version(void);
+int nk_opts_default(nk_opts* o);
+const char* nk_status_string(int code);
+
+/* ---------------- discrete operators (sh_scipy_nk.py:31-49; main.cpp:19-81) ---------------- */
+
+/* y = Lap v, periodic 5-point Laplacian, e = 1/h^2.  Replaces the CSR SpMV `Lap @ v`
+ * (sh_scipy_nk.py:32-35; Eigen SpMV over main.cpp:38-71). */
+int nk_lap5_apply(const double* v_dev, double* y_dev, int64_t ny, int64_t nx, double e, void* stream);
+
+/* y = L v, L = -Lap*Lap - 2*Lap + (r-1)*I as a 13-point periodic stencil.  Replaces `L @ u`
+ * (sh_scipy_nk.py:38-39,49; main.cpp:23-24,78-81). */
+int nk_sh13_apply(const double* v_dev, double* y_dev, int64_t ny, int64_t nx, double h, double r,
+                  void* stream);
+
+/* F = (u-uo)/k - (L u + g u^2 - u^3 + L uo + g uo^2 - uo^3)/2, the reference residual
+ * (sh_scipy_nk.py:47-49; main.cpp:19-32), evaluated in one fused pass. */
+int nk_sh_residual(const double* u_dev, const double* uo_dev, double* F_dev, int64_t ny, int64_t nx,
+                   double h, double r, double k, double g, void* stream);
+
+/* y = J(u) v = v/k - (L v + (2 g u - 3 u^2) v)/2 (analytic Jacobian of the residual above). */
+int nk_sh_jvp(const double* u_dev, const double* v_dev, double* y_dev, int64_t ny, int64_t nx,
+              double h, double r, double k, double g, void* stream);
+
+/* ---------------- BLAS-1 (scipy get_blas_funcs dot/nrm2/axpy/scal in _gcrotmk.py:104-126) ------ */
+/* Scalar results are written to host memory; the call synchronises `stream`. */
+int nk_dot(const double* x_dev, const double* y_dev, int64_t n, double* out, void* stream);
+int nk_nrm2(const double* x_dev, int64_t n, double* out, void* stream);
+int nk_maxnorm(const double* x_dev, int64_t n, double* out, void* stream); /* _nonlin.py:36-37 */
+int nk_axpy(double a, const double* x_dev, double* y_dev, int64_t n, void* stream);
+int nk_scal(double a, double* x_dev, int64_t n, void* stream);
+/* out[i] = V[i] . w for i < m, in one pass over w (V: host array of m device pointers). */
+int nk_mdot(const double* const* V_dev, int32_t m, const double* w_dev, int64_t n, double* out,
+            void* stream);
+/* y += sum_i coef[i] * V[i] in one pass (coef: host array). */
+int nk_maxpy(const double* const* V_dev, const double* coef, int32_t m, double* y_dev, int64_t n,
+             void* stream);
+
+/* ---------------- communicators (row-slab decomposition over RCCL / xGMI) ---------------- */
+int nk_comm_unique_id_bytes(void);
+int nk_comm_get_unique_id(void* out);
+/* One process per GPU: RCCL communicator from a unique id shared by rank 0. */
+int nk_comm_create_rccl(nk_comm** out, const void* unique_id, int32_t rank, int32_t nranks);
+/* One process, `nranks` slabs driven by `nranks` host threads on one device (testing the slab
+ * logic on a single GPU): fills out[0..nranks-1]. */
+int nk_comm_create_loopback(nk_comm** out, int32_t nranks);
+int nk_comm_destroy(nk_comm* c);
+
+/* ---------------- Swift-Hohenberg implicit time step (the north-star path) ---------------- */
+/* A stepper for one row slab [row0, row0+ny_local) of an ny_global x nx periodic grid.
+ * comm == NULL means a single slab (ny_local == ny_global).  Replaces the loop body
+ * sh_scipy_nk.py:56-61 (`U = newton_krylov(residual, Uo)`) and main.cpp:97-104
+ * (`U = nonlin_solve(residual, Uo, 6e-6, inf, inf, inf)`). */
+int nk_sh_create(nk_sh** out, int64_t ny_local, int64_t nx, int64_t ny_global, double h, double r,
+                 double k, double g, const nk_opts* opts, nk_comm* comm, void* stream);
+int nk_sh_destroy(nk_sh* s);
+/* u_next = the Crank-Nicolson step from u_prev (both local slabs, may alias). */
+int nk_sh_step(nk_sh* s, const double* u_prev_dev, double* u_next_dev, nk_stats* stats);
+int nk_sh_set_opts(nk_sh* s, const nk_opts* opts);
+/* Copies up to `max` per-kernel-class records; returns the number of classes. */
+int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max);
+int nk_sh_reset_profile(nk_sh* s);
+int64_t nk_sh_workspace_bytes(nk_sh* s);
+
+/* ---------------- generic drop-in: newton_krylov(F, xin) over a device residual ---------------- */
+/* F(ctx, x_dev, f_dev, n) evaluates the residual on device buffers and returns 0 on success.
+ * Replaces scipy.optimize.newton_krylov (scipy/optimize/_nonlin.py:1603) for any residual, e.g.
+ * the droplet / PMA2 closures (droplet.py:383, PMA2_nk.py:100). */
+/* `workspace` (device, 256-B aligned, nk_solve_workspace_bytes() long) may be NULL, in which case
+ * the solver allocates it; every pointer handed to F points into the workspace or x0/x. */
+typedef int (*nk_residual_fn)(void* ctx, const double* x_dev, double* f_dev, int64_t n);
+int64_t nk_solve_workspace_bytes(int64_t n, const nk_opts* opts);
+int nk_solve(nk_residual_fn F, void* ctx, const double* x0_dev, double* x_dev, int64_t n,
+             const nk_opts* opts, nk_stats* stats, void* stream, void* workspace,
+             int64_t workspace_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NKHIP_H */

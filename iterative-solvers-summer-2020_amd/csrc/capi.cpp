@@ -1,0 +1,327 @@
+// extern "C" boundary of libnkhip (declared in include/nkhip.h).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+
+#include "../../include/nkhip.h"
+#include "comm.h"
+#include "nk_kernels.h"
+#include "nk_solver.h"
+#include "sh_problem.h"
+
+using namespace nk;
+
+namespace {
+
+hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+int hip_rc(hipError_t e) {
+  if (e == hipSuccess) return NK_OK;
+  std::fprintf(stderr, "nkhip: HIP error %d (%s)\n", int(e), hipGetErrorString(e));
+  return NK_EHIP;
+}
+
+// Runs a kernel that leaves per-block partials, then reduces them into host `out`.
+template <class L>
+int reduce_call(int64_t n, int nslots, int nsum, int nv, double* out, hipStream_t s, L&& fn) {
+  const int64_t kb = krylov_blocks(n) + 1;
+  double* buf = nullptr;
+  const size_t bytes = sizeof(double) * (size_t(kb) * nslots + nv);
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), bytes, s);
+  if (e != hipSuccess) return hip_rc(e);
+  int64_t nblk = 0;
+  e = fn(buf, &nblk);
+  double* res = buf + size_t(kb) * nslots;
+  if (e == hipSuccess) e = reduce_final_launch(buf, nblk, nsum, nv, res, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, res, sizeof(double) * nv, hipMemcpyDeviceToHost, s);
+  hipFreeAsync(buf, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  return hip_rc(e);
+}
+
+}  // namespace
+
+struct nk_sh {
+  std::unique_ptr<Engine> E;
+  std::unique_ptr<SHProblem> P;
+  std::unique_ptr<NewtonKrylov> NK;
+  nk_opts opts;
+  int64_t ny, nx;
+};
+
+extern "C" {
+
+const char* nk_version(void) { return "nkhip 0.1.0 (gfx950)"; }
+
+int nk_opts_default(nk_opts* o) {
+  if (!o) return NK_EINVAL;
+  *o = default_opts();
+  return NK_OK;
+}
+
+const char* nk_status_string(int code) {
+  switch (code) {
+    case NK_OK: return "ok";
+    case NK_NO_CONVERGENCE: return "no convergence (maxiter reached)";
+    case NK_NONFINITE: return "Function returned non-finite results";
+    case NK_ZERO_STEP:
+      return "Jacobian inversion yielded zero vector. This indicates a bug in the Jacobian "
+             "approximation.";
+    case NK_EINVAL: return "invalid argument";
+    case NK_EHIP: return "HIP runtime error";
+    case NK_ECOMM: return "RCCL error";
+    case NK_ENOMEM: return "out of device memory";
+  }
+  return "unknown status";
+}
+
+// ------------------------------------------------------------------------------ operators
+int nk_lap5_apply(const double* v, double* y, int64_t ny, int64_t nx, double e, void* stream) {
+  if (!v || !y || ny <= 0 || nx <= 0) return NK_EINVAL;
+  StencilArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.a = periodic(v);
+  A.out0 = y;
+  A.e = e;
+  return hip_rc(stencil_launch(SMode::LAP5, A, S(stream), nullptr));
+}
+
+int nk_sh13_apply(const double* v, double* y, int64_t ny, int64_t nx, double h, double r,
+                  void* stream) {
+  if (!v || !y || ny <= 0 || nx <= 0) return NK_EINVAL;
+  StencilArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.a = periodic(v);
+  A.out0 = y;
+  A.c = sh_coef(h, r, 1.0, 0.0);
+  return hip_rc(stencil_launch(SMode::SH13, A, S(stream), nullptr));
+}
+
+int nk_sh_residual(const double* u, const double* uo, double* F, int64_t ny, int64_t nx, double h,
+                   double r, double k, double g, void* stream) {
+  if (!u || !uo || !F || ny <= 0 || nx <= 0) return NK_EINVAL;
+  StencilArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.a = periodic(u);
+  A.b = periodic(uo);
+  A.out0 = F;
+  A.c = sh_coef(h, r, k, g);
+  return hip_rc(stencil_launch(SMode::RESID, A, S(stream), nullptr));
+}
+
+int nk_sh_jvp(const double* u, const double* v, double* y, int64_t ny, int64_t nx, double h,
+              double r, double k, double g, void* stream) {
+  if (!u || !v || !y || ny <= 0 || nx <= 0) return NK_EINVAL;
+  StencilArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.a = periodic(v);
+  A.p0 = u;
+  A.alpha = 1.0;
+  A.out0 = y;
+  A.c = sh_coef(h, r, k, g);
+  return hip_rc(stencil_launch(SMode::AJVP, A, S(stream), nullptr));
+}
+
+// ------------------------------------------------------------------------------ BLAS-1
+int nk_dot(const double* x, const double* y, int64_t n, double* out, void* stream) {
+  if (!x || !y || !out || n < 0) return NK_EINVAL;
+  VecList P;
+  P.p[0] = y;
+  return reduce_call(n, 3, 3, 1, out, S(stream), [&](double* part, int64_t* nb) {
+    return mdot_launch(x, nullptr, P, 1, n, part, S(stream), nb);
+  });
+}
+
+int nk_nrm2(const double* x, int64_t n, double* out, void* stream) {
+  if (!x || !out || n < 0) return NK_EINVAL;
+  double s2 = 0.0;
+  VecList P;
+  P.p[0] = x;
+  const int rc = reduce_call(n, 3, 3, 1, &s2, S(stream), [&](double* part, int64_t* nb) {
+    return mdot_launch(x, nullptr, P, 1, n, part, S(stream), nb);
+  });
+  *out = std::sqrt(s2);
+  return rc;
+}
+
+int nk_maxnorm(const double* x, int64_t n, double* out, void* stream) {
+  if (!x || !out || n <= 0) return NK_EINVAL;
+  // combo with no vectors: out = 1*x (written to scratch), partial [sum x^2, max|x|]
+  double* tmp = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tmp), sizeof(double) * n, S(stream));
+  if (e != hipSuccess) return hip_rc(e);
+  VecList none;
+  double r2[2];
+  const int rc = reduce_call(n, 2, 1, 2, r2, S(stream), [&](double* part, int64_t* nb) {
+    return combo_launch(tmp, x, 1.0, none, 0, n, part, S(stream), nb);
+  });
+  hipFreeAsync(tmp, S(stream));
+  hipStreamSynchronize(S(stream));
+  *out = r2[1];
+  return rc;
+}
+
+int nk_axpy(double a, const double* x, double* y, int64_t n, void* stream) {
+  if (!x || !y || n < 0) return NK_EINVAL;
+  return hip_rc(axpby_launch(a, x, 1.0, y, y, n, S(stream)));
+}
+
+int nk_scal(double a, double* x, int64_t n, void* stream) {
+  if (!x || n < 0) return NK_EINVAL;
+  return hip_rc(axpby_launch(a, x, 0.0, nullptr, x, n, S(stream)));
+}
+
+int nk_mdot(const double* const* V, int32_t m, const double* w, int64_t n, double* out,
+            void* stream) {
+  if (!V || !w || !out || m < 0 || m > kMaxVec || n < 0) return NK_EINVAL;
+  if (m == 0) return NK_OK;
+  VecList P;
+  for (int i = 0; i < m; ++i) P.p[i] = V[i];
+  const int nv = 2 * m + 1;
+  double res[2 * kMaxVec + 1];
+  const int rc = reduce_call(n, nv, nv, nv, res, S(stream), [&](double* part, int64_t* nb) {
+    return mdot_launch(w, nullptr, P, m, n, part, S(stream), nb);
+  });
+  for (int i = 0; i < m; ++i) out[i] = res[i];
+  return rc;
+}
+
+int nk_maxpy(const double* const* V, const double* coef, int32_t m, double* y, int64_t n,
+             void* stream) {
+  if (!V || !coef || !y || m < 0 || m > kMaxVec || n < 0) return NK_EINVAL;
+  VecList P;
+  for (int i = 0; i < m; ++i) {
+    P.p[i] = V[i];
+    P.c[i] = coef[i];
+  }
+  int64_t nb = 0;
+  return hip_rc(combo_launch(y, y, 1.0, P, m, n, nullptr, S(stream), &nb));
+}
+
+// ------------------------------------------------------------------------------ comms
+int nk_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
+int nk_comm_get_unique_id(void* out) { return out ? comm_get_unique_id(out) : NK_EINVAL; }
+int nk_comm_create_rccl(nk_comm** out, const void* uid, int32_t rank, int32_t nranks) {
+  return comm_create_rccl(out, uid, rank, nranks);
+}
+int nk_comm_create_loopback(nk_comm** out, int32_t nranks) {
+  return comm_create_loopback(out, nranks);
+}
+int nk_comm_destroy(nk_comm* c) {
+  delete c;
+  return NK_OK;
+}
+
+// ------------------------------------------------------------------------------ SH stepper
+int nk_sh_create(nk_sh** out, int64_t ny_local, int64_t nx, int64_t ny_global, double h, double r,
+                 double k, double g, const nk_opts* opts, nk_comm* comm, void* stream) {
+  if (!out || ny_local <= 0 || nx <= 0 || ny_global < ny_local || !(h > 0) || !(k != 0))
+    return NK_EINVAL;
+  if (comm && comm->size() > 1 && ny_local < 2) return NK_EINVAL;
+  if ((!comm || comm->size() == 1) && ny_global != ny_local) return NK_EINVAL;
+  std::unique_ptr<nk_sh> sh(new (std::nothrow) nk_sh());
+  if (!sh) return NK_ENOMEM;
+  sh->opts = opts ? *opts : default_opts();
+  sh->ny = ny_local;
+  sh->nx = nx;
+  sh->E = std::make_unique<Engine>(ny_local * nx, comm, S(stream), sh->opts.profile != 0,
+                                   stencil_partial_slots(ny_local, nx));
+  sh->P = std::make_unique<SHProblem>(*sh->E, ny_local, nx, ny_global, sh_coef(h, r, k, g),
+                                      sh->opts.jvp_mode);
+  if (sh->P->status()) return sh->P->status();
+  sh->NK = std::make_unique<NewtonKrylov>(*sh->E, *sh->P, sh->opts);
+  if (sh->NK->status()) return sh->NK->status();
+  const int rc = sh->E->sync();
+  if (rc) return rc;
+  *out = sh.release();
+  return NK_OK;
+}
+
+int nk_sh_destroy(nk_sh* s) {
+  delete s;
+  return NK_OK;
+}
+
+int nk_sh_set_opts(nk_sh* s, const nk_opts* opts) {
+  if (!s || !opts) return NK_EINVAL;
+  if (opts->inner_m != s->opts.inner_m || opts->outer_k != s->opts.outer_k) return NK_EINVAL;
+  s->opts = *opts;
+  s->E->profile = opts->profile != 0;
+  s->P->set_jvp_mode(opts->jvp_mode);
+  s->NK->set_opts(*opts);
+  return NK_OK;
+}
+
+int nk_sh_step(nk_sh* s, const double* u_prev, double* u_next, nk_stats* stats) {
+  if (!s || !u_prev || !u_next) return NK_EINVAL;
+  int rc = s->P->prepare(u_prev);
+  if (rc) return rc;
+  return s->NK->solve(u_prev, u_next, stats);
+}
+
+int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {
+  static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
+                                         "krylov_mdot", "krylov_combo", "reduce_final", "copy",
+                                         "halo", "user_F", "axpby"};
+  if (!s) return NK_EINVAL;
+  for (int k = 0; k < K_NKINDS && k < max; ++k) {
+    std::memset(out[k].name, 0, sizeof(out[k].name));
+    std::strncpy(out[k].name, names[k], sizeof(out[k].name) - 1);
+    out[k].launches = s->E->stat(k).launches;
+    out[k].total_ms = s->E->stat(k).ms;
+    out[k].alg_bytes = s->E->stat(k).bytes;
+  }
+  return K_NKINDS;
+}
+
+int nk_sh_reset_profile(nk_sh* s) {
+  if (!s) return NK_EINVAL;
+  s->E->reset_stats();
+  return NK_OK;
+}
+
+int64_t nk_sh_workspace_bytes(nk_sh* s) { return s ? s->E->bytes_allocated() : -1; }
+
+// ------------------------------------------------------------------------------ generic
+int64_t nk_solve_workspace_bytes(int64_t n, const nk_opts* opts) {
+  if (n <= 0) return NK_EINVAL;
+  const nk_opts o = opts ? *opts : default_opts();
+  return int64_t(sizeof(double)) * Engine::pad(n) * (NewtonKrylov::vectors_needed(o) + 2);
+}
+
+int nk_solve(nk_residual_fn F, void* ctx, const double* x0, double* x, int64_t n,
+             const nk_opts* opts, nk_stats* stats, void* stream, void* workspace,
+             int64_t workspace_bytes) {
+  if (!F || !x0 || !x || n <= 0) return NK_EINVAL;
+  const nk_opts o = opts ? *opts : default_opts();
+  if (o.jvp_mode != NK_JVP_FD) return NK_EINVAL;  // a user residual has no analytic Jacobian
+  Engine E(n, nullptr, S(stream), o.profile != 0);
+  const int nvec = NewtonKrylov::vectors_needed(o);
+  const int64_t npad = Engine::pad(n);
+  const int64_t need = nk_solve_workspace_bytes(n, &o);
+  double* ws = static_cast<double*>(workspace);
+  const bool own = (ws == nullptr);
+  if (!own && (workspace_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255u)))
+    return NK_EINVAL;
+  if (own && hipMalloc(reinterpret_cast<void**>(&ws), need) != hipSuccess) return NK_ENOMEM;
+  CallbackProblem P(E, F, ctx, ws + npad * nvec, ws + npad * (nvec + 1));
+  int rc;
+  {
+    NewtonKrylov NK(E, P, o, ws, int64_t(sizeof(double)) * npad * nvec);
+    rc = NK.status();
+    if (!rc) rc = NK.solve(x0, x, stats);
+  }
+  hipStreamSynchronize(S(stream));
+  if (own) hipFree(ws);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,186 @@
+// Communicators for the row-slab decomposition (see comm.h).
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/nkhip.h"
+
+namespace nk {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// RCCL: one process per GPU.  Halo = grouped ncclSend/ncclRecv with the ring neighbours on the
+// solver's stream; reductions = ncclAllReduce in place on the device result vector.
+// ------------------------------------------------------------------------------------------
+struct RcclComm final : nk_comm {
+  ncclComm_t c = nullptr;
+  int r = 0, p = 1;
+  ~RcclComm() override {
+    if (c) ncclCommDestroy(c);
+  }
+  int rank() const override { return r; }
+  int size() const override { return p; }
+
+  int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) override {
+    if (nsum > 0 && ncclAllReduce(dev, dev, size_t(nsum), ncclDouble, ncclSum, c, s) != ncclSuccess)
+      return NK_ECOMM;
+    if (nv > nsum &&
+        ncclAllReduce(dev + nsum, dev + nsum, size_t(nv - nsum), ncclDouble, ncclMax, c, s) !=
+            ncclSuccess)
+      return NK_ECOMM;
+    if (hipMemcpyAsync(host, dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return NK_EHIP;
+    return hipStreamSynchronize(s) == hipSuccess ? NK_OK : NK_EHIP;
+  }
+
+  int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
+           hipStream_t s) override {
+    const int prev = (r - 1 + p) % p, next = (r + 1) % p;
+    const size_t cnt = size_t(2 * nx);
+    // Sends to one peer are matched in posting order, so with p == 2 (prev == next) the
+    // neighbour's first receive (its lo) gets our last rows and its second (its hi) our first.
+    if (ncclGroupStart() != ncclSuccess) return NK_ECOMM;
+    ncclSend(v + (ny - 2) * nx, cnt, ncclDouble, next, c, s);
+    ncclSend(v, cnt, ncclDouble, prev, c, s);
+    ncclRecv(lo, cnt, ncclDouble, prev, c, s);
+    ncclRecv(hi, cnt, ncclDouble, next, c, s);
+    return ncclGroupEnd() == ncclSuccess ? NK_OK : NK_ECOMM;
+  }
+
+  int barrier(hipStream_t s) override {
+    double* d = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double), s) != hipSuccess) return NK_EHIP;
+    hipMemsetAsync(d, 0, sizeof(double), s);
+    const ncclResult_t e = ncclAllReduce(d, d, 1, ncclDouble, ncclSum, c, s);
+    hipFreeAsync(d, s);
+    if (e != ncclSuccess) return NK_ECOMM;
+    return hipStreamSynchronize(s) == hipSuccess ? NK_OK : NK_EHIP;
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// Loopback: `p` slabs on one device, each driven by its own host thread.  Halos are D2D copies
+// from the neighbour's slab after a host barrier; reductions are combined on the host in rank
+// order (deterministic).  Used to test the slab decomposition on a single GPU.
+// ------------------------------------------------------------------------------------------
+struct LoopShared {
+  int p;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  int64_t gen = 0;
+  std::vector<const double*> vptr;
+  std::vector<int64_t> vny;
+  std::vector<std::vector<double>> vals;
+  explicit LoopShared(int np) : p(np), vptr(np), vny(np), vals(np) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(m);
+    const int64_t g = gen;
+    if (++arrived == p) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+struct LoopComm final : nk_comm {
+  std::shared_ptr<LoopShared> sh;
+  int r = 0;
+  int rank() const override { return r; }
+  int size() const override { return sh->p; }
+
+  int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) override {
+    if (hipMemcpyAsync(host, dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return NK_EHIP;
+    sh->vals[r].assign(host, host + nv);
+    sh->wait();
+    for (int k = 0; k < nv; ++k) {
+      double acc = sh->vals[0][k];
+      for (int q = 1; q < sh->p; ++q) {
+        const double v = sh->vals[q][k];
+        if (k < nsum)
+          acc += v;
+        else if (acc == acc && (v != v || v > acc))
+          acc = v;
+      }
+      host[k] = acc;
+    }
+    sh->wait();
+    return NK_OK;
+  }
+
+  int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
+           hipStream_t s) override {
+    const int p = sh->p, prev = (r - 1 + p) % p, next = (r + 1) % p;
+    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+    sh->vptr[r] = v;
+    sh->vny[r] = ny;
+    sh->wait();
+    const size_t bytes = sizeof(double) * size_t(2 * nx);
+    hipError_t e = hipMemcpyAsync(lo, sh->vptr[prev] + (sh->vny[prev] - 2) * nx, bytes,
+                                  hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(hi, sh->vptr[next], bytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    sh->wait();  // nobody may overwrite its slab before every neighbour has copied
+    return e == hipSuccess ? NK_OK : NK_EHIP;
+  }
+
+  int barrier(hipStream_t s) override {
+    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+    sh->wait();
+    return NK_OK;
+  }
+};
+
+}  // namespace
+
+int comm_unique_id_bytes() { return int(sizeof(ncclUniqueId)); }
+
+int comm_get_unique_id(void* out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return NK_ECOMM;
+  std::memcpy(out, &id, sizeof(id));
+  return NK_OK;
+}
+
+int comm_create_rccl(nk_comm** out, const void* uid, int rank, int nranks) {
+  if (!out || !uid || nranks < 1 || rank < 0 || rank >= nranks) return NK_EINVAL;
+  auto c = std::make_unique<RcclComm>();
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  const ncclResult_t e = ncclCommInitRank(&c->c, nranks, id, rank);
+  if (e != ncclSuccess) {
+    std::fprintf(stderr, "nkhip: ncclCommInitRank failed: %s\n", ncclGetErrorString(e));
+    c->c = nullptr;
+    return NK_ECOMM;
+  }
+  c->r = rank;
+  c->p = nranks;
+  *out = c.release();
+  return NK_OK;
+}
+
+int comm_create_loopback(nk_comm** out, int nranks) {
+  if (!out || nranks < 1) return NK_EINVAL;
+  auto sh = std::make_shared<LoopShared>(nranks);
+  for (int q = 0; q < nranks; ++q) {
+    auto c = new LoopComm();
+    c->sh = sh;
+    c->r = q;
+    out[q] = c;
+  }
+  return NK_OK;
+}
+
+}  // namespace nk

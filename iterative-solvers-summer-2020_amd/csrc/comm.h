@@ -1,0 +1,33 @@
+// Row-slab communicators: RCCL over xGMI (one process per GPU) and a loopback group (several
+// slabs on one GPU, one host thread each) that exercises the same slab logic on a single device.
+//
+// The reference has no distributed code at all; the exchange pattern is
+// the one the periodic 13-point stencil needs: a 2-row halo with the up/down ring neighbours per
+// stencil pass, plus small all-reduces (sum for dots / norms, max for the max-norm of
+// TerminationCondition, scipy/optimize/_nonlin.py:354).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+struct nk_comm {
+  virtual ~nk_comm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  // dev[0, nsum) summed and dev[nsum, nv) max-reduced over ranks; the result lands in host[0, nv).
+  // Synchronises `s`.  Returns 0 or a negative NK_E* code.
+  virtual int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) = 0;
+  // lo <- rows ny_prev-2, ny_prev-1 of the previous rank, hi <- rows 0, 1 of the next rank
+  // (periodic ring).  Enqueued on `s` (RCCL) or completed before return (loopback).
+  virtual int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
+                   hipStream_t s) = 0;
+  virtual int barrier(hipStream_t s) = 0;
+};
+
+namespace nk {
+int comm_unique_id_bytes();
+int comm_get_unique_id(void* out);
+int comm_create_rccl(nk_comm** out, const void* uid, int rank, int nranks);
+int comm_create_loopback(nk_comm** out, int nranks);
+}  // namespace nk

@@ -1,0 +1,249 @@
+// Krylov BLAS-1 kernels for the Arnoldi process (gfx950, wave64).
+//
+// Replaces the per-vector BLAS dot/axpy/nrm2/scal loop of SciPy's MGS Arnoldi
+// (scipy/sparse/linalg/_isolve/_gcrotmk.py:104-143) with two fused passes per Arnoldi step:
+//   mdot  -- all inner products V^T w (and the new Gram row V^T v_j, and w.w) in ONE read of
+//            w and the basis, partial sums per block;
+//   combo -- w <- w - sum_i c_i v_i together with |w|^2 and max|w| in ONE read-modify-write.
+// A block owns a contiguous 2048-element chunk (256 threads x 4 double2), keeps its chunk of w
+// in registers and streams the basis vectors through it; reductions are wave64 xor-shuffles, one
+// LDS round, then a deterministic second-stage kernel (fixed summation order, so a run is
+// bit-reproducible).
+#include <cmath>
+
+#include "nk_device.h"
+#include "nk_kernels.h"
+
+namespace nk {
+namespace {
+
+constexpr int BS = kKrylovBlock;
+constexpr int PAIRS = kKrylovPerThread / 2;  // double2 per thread and vector
+
+template <bool VEC>
+__device__ __forceinline__ double2 ld2(const double* p, int64_t i, int64_t n) {
+  if (VEC && i + 1 < n) return *reinterpret_cast<const double2*>(p + i);
+  double2 r;
+  r.x = (i < n) ? p[i] : 0.0;
+  r.y = (i + 1 < n) ? p[i + 1] : 0.0;
+  return r;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void st2(double* p, int64_t i, int64_t n, double2 v) {
+  if (VEC && i + 1 < n) {
+    *reinterpret_cast<double2*>(p + i) = v;
+    return;
+  }
+  if (i < n) p[i] = v.x;
+  if (i + 1 < n) p[i + 1] = v.y;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double* g, VecList P,
+                                                  int np, int64_t n, double* partial) {
+  const int64_t nblk = gridDim.x;
+  const int64_t bid = blockIdx.x;
+  const int64_t base = bid * kKrylovChunk + 2 * int64_t(threadIdx.x);
+  double2 av[PAIRS], gv[PAIRS];
+  double aa = 0.0;
+#pragma unroll
+  for (int k = 0; k < PAIRS; ++k) {
+    av[k] = ld2<VEC>(a, base + k * 2 * BS, n);
+    gv[k] = g ? ld2<VEC>(g, base + k * 2 * BS, n) : make_double2(0.0, 0.0);
+    aa += av[k].x * av[k].x + av[k].y * av[k].y;
+  }
+  int buf = 0;
+  for (int i0 = 0; i0 < np; i0 += 4) {
+    double s[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u < np) {
+        const double* p = P.p[i0 + u];
+        double2 pv[PAIRS];
+        if (p == g) {  // the Gram-row vector is already in registers: no second read
+#pragma unroll
+          for (int k = 0; k < PAIRS; ++k) pv[k] = gv[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
+        }
+#pragma unroll
+        for (int k = 0; k < PAIRS; ++k) {
+          s[u] += av[k].x * pv[k].x + av[k].y * pv[k].y;
+          s[4 + u] += gv[k].x * pv[k].x + gv[k].y * pv[k].y;
+        }
+      }
+    }
+    const double v = block_reduce<8, 8, BS>(s, buf);
+    buf ^= 1;
+    if (threadIdx.x < 8) {
+      const int u = threadIdx.x & 3;
+      if (i0 + u < np) {
+        const int64_t slot = (threadIdx.x < 4) ? (i0 + u) : (np + i0 + u);
+        partial[slot * nblk + bid] = v;
+      }
+    }
+  }
+  double t[1] = {aa};
+  const double v = block_reduce<1, 1, BS>(t, buf);
+  if (threadIdx.x == 0) partial[int64_t(2 * np) * nblk + bid] = v;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
+                                                   VecList P, int np, int64_t n,
+                                                   double* partial) {
+  const int64_t nblk = gridDim.x;
+  const int64_t bid = blockIdx.x;
+  const int64_t base = bid * kKrylovChunk + 2 * int64_t(threadIdx.x);
+  double2 acc[PAIRS];
+#pragma unroll
+  for (int k = 0; k < PAIRS; ++k) {
+    if (in) {
+      const double2 x = ld2<VEC>(in, base + k * 2 * BS, n);
+      acc[k] = make_double2(cin * x.x, cin * x.y);
+    } else {
+      acc[k] = make_double2(0.0, 0.0);
+    }
+  }
+#pragma unroll 2
+  for (int i = 0; i < np; ++i) {
+    const double* p = P.p[i];
+    const double c = P.c[i];
+    double2 pv[PAIRS];
+#pragma unroll
+    for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
+#pragma unroll
+    for (int k = 0; k < PAIRS; ++k) {
+      acc[k].x += c * pv[k].x;
+      acc[k].y += c * pv[k].y;
+    }
+  }
+  double red[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < PAIRS; ++k) {
+    st2<VEC>(out, base + k * 2 * BS, n, acc[k]);
+    const int64_t i = base + k * 2 * BS;
+    if (i < n) {
+      red[0] += acc[k].x * acc[k].x;
+      red[1] = nmax(red[1], fabs(acc[k].x));
+    }
+    if (i + 1 < n) {
+      red[0] += acc[k].y * acc[k].y;
+      red[1] = nmax(red[1], fabs(acc[k].y));
+    }
+  }
+  if (partial) {
+    const double v = block_reduce<2, 1, BS>(red);
+    if (threadIdx.x < 2) partial[int64_t(threadIdx.x) * nblk + bid] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial, int64_t nblk,
+                                                           int nsum, double* result) {
+  const int k = blockIdx.x;
+  const bool is_sum = k < nsum;
+  const double* p = partial + int64_t(k) * nblk;
+  double acc = 0.0;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
+  double v[1] = {acc};
+  // the reduction tree is fixed, so the result does not depend on timing
+  double s = 0.0;
+  if (is_sum) {
+    s = block_reduce<1, 1, 256>(v);
+  } else {
+    s = block_reduce<1, 0, 256>(v);
+  }
+  if (threadIdx.x == 0) result[k] = s;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) axpby_kernel(double a, const double* x, double b,
+                                                    const double* y, double* out, int64_t n) {
+  const int64_t i = 2 * (int64_t(blockIdx.x) * 256 + threadIdx.x);
+  if (i >= n) return;
+  const double2 xv = ld2<VEC>(x, i, n);
+  double2 r = make_double2(a * xv.x, a * xv.y);
+  if (y) {
+    const double2 yv = ld2<VEC>(y, i, n);
+    r.x += b * yv.x;
+    r.y += b * yv.y;
+  }
+  st2<VEC>(out, i, n, r);
+}
+
+__global__ void __launch_bounds__(256) fddiff_kernel(double* w, const double* f0, double sc,
+                                                     int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) w[i] = (w[i] - f0[i]) / sc;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
+                       double* partial, hipStream_t s, int64_t* nblk) {
+  if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
+  const int64_t nb = krylov_blocks(n);
+  if (nblk) *nblk = nb;
+  if (nb == 0) return hipSuccess;
+  bool vec = al16(a) && al16(g);
+  for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
+  if (vec)
+    hipLaunchKernelGGL(mdot_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n,
+                       partial);
+  else
+    hipLaunchKernelGGL(mdot_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n,
+                       partial);
+  return hipGetLastError();
+}
+
+hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
+                        int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
+  if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
+  const int64_t nb = krylov_blocks(n);
+  if (nblk) *nblk = nb;
+  if (nb == 0) return hipSuccess;
+  bool vec = al16(out) && al16(in);
+  for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
+  if (vec)
+    hipLaunchKernelGGL(combo_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
+                       np, n, partial);
+  else
+    hipLaunchKernelGGL(combo_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
+                       np, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,
+                               double* result, hipStream_t s) {
+  if (nv <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_final_kernel, dim3(unsigned(nv)), dim3(256), 0, s, partial, nblk, nsum,
+                     result);
+  return hipGetLastError();
+}
+
+hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
+                        int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t g = (n + 511) / 512;
+  const bool vec = al16(x) && al16(y) && al16(out);
+  if (vec)
+    hipLaunchKernelGGL(axpby_kernel<true>, dim3(unsigned(g)), dim3(256), 0, s, a, x, b, y, out, n);
+  else
+    hipLaunchKernelGGL(axpby_kernel<false>, dim3(unsigned(g)), dim3(256), 0, s, a, x, b, y, out,
+                       n);
+  return hipGetLastError();
+}
+
+hipError_t fddiff_launch(double* w, const double* f0, double sc, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fddiff_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, w, f0, sc, n);
+  return hipGetLastError();
+}
+
+}  // namespace nk

@@ -1,0 +1,49 @@
+// Device-side helpers shared by the stencil and Krylov kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace nk {
+
+// NaN-propagating max, so that max|F| of a vector holding a NaN is NaN (numpy abs(x).max()).
+__device__ __forceinline__ double nmax(double a, double b) {
+  if (a != a) return a;
+  return (b != b || b > a) ? b : a;
+}
+
+// Reduce NV values over a 1-D block of BS threads: the first NSUM values are summed, the rest
+// max-reduced (NaN-propagating).  Wave64 xor-shuffle tree, then one LDS round across waves.
+// Returns value `threadIdx.x` to the threads with threadIdx.x < NV (others get 0).
+// `buf` selects one of two LDS buffers so that back-to-back calls need one barrier each.
+template <int NV, int NSUM, int BS>
+__device__ __forceinline__ double block_reduce(double (&v)[NV], int buf = 0) {
+  static_assert(BS % 64 == 0, "block must be whole waves");
+  constexpr int NW = BS / 64;
+  __shared__ double sm[2][NV][NW];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double t = __shfl_xor(v[k], o, 64);
+      v[k] = (k < NSUM) ? v[k] + t : nmax(v[k], t);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sm[buf][k][wid] = v[k];
+  }
+  __syncthreads();
+  double acc = 0.0;
+  if (threadIdx.x < NV) {
+    const int k = threadIdx.x;
+    acc = sm[buf][k][0];
+    for (int w = 1; w < NW; ++w) acc = (k < NSUM) ? acc + sm[buf][k][w] : nmax(acc, sm[buf][k][w]);
+  }
+  return acc;
+}
+
+}  // namespace nk

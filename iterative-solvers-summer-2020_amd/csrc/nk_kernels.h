@@ -1,0 +1,92 @@
+// Internal kernel interface of libnkhip (not part of the C-ABI).
+//
+// Layout in HBM: every grid vector is one row-major fp64 array u[i*nx + j] over the rank's row
+// slab (i = y, j = x; sh_scipy_nk.py:34-35 fixes the flattening).  Stencil inputs carry two halo
+// rows on each side: `lo` = global rows row0-2, row0-1 and `hi` = rows row0+ny, row0+ny+1, each a
+// contiguous 2*nx block.  A single slab (one GPU) wraps periodically instead (lo == nullptr).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace nk {
+
+// ---------------------------------------------------------------------------------------------
+struct Field {
+  const double* base;  // rows [0, ny)
+  const double* lo;    // rows -2, -1   (nullptr: periodic wrap on base)
+  const double* hi;    // rows ny, ny+1
+};
+
+inline Field periodic(const double* p) { return Field{p, nullptr, nullptr}; }
+
+// 13-point coefficients of L = -Lap^2 - 2 Lap + (r-1) I with e = 1/h^2 (sh_scipy_nk.py:32,38-39).
+struct SHCoef {
+  double c0, c1, c2, c3;  // centre, axial +-1, diagonal, axial +-2
+  double k, g;            // time step, quadratic coefficient (sh_scipy_nk.py:18,29)
+};
+SHCoef sh_coef(double h, double r, double k, double g);
+
+enum class SMode : int {
+  LAP5 = 0,   // out0 = Lap a                                     (sh_scipy_nk.py:32-35)
+  SH13 = 1,   // out0 = L a                                       (sh_scipy_nk.py:38-39)
+  RESID = 2,  // out0 = F(a; uo = b), the reference residual       (sh_scipy_nk.py:47-49)
+  BOLD = 3,   // out0 = B(uo = a) = -uo/k - (L uo + g uo^2 - uo^3)/2, so F(u) = G(u) + B
+  TRIAL = 4,  // w = a + alpha b: out2 = w, out1 = G(w), out0 = G(w) + p0; sums |F|^2, max|F|, max|w|
+  FDJVP = 5,  // w = a + alpha b: out0 = (G(w) - p0) / sc          (_nonlin.py:1505-1513)
+  AJVP = 6,   // out0 = alpha*(a/k - (L a + (2 g u - 3 u^2) a)/2) with u = p0 (analytic J v)
+};
+
+struct StencilArgs {
+  int64_t ny = 0, nx = 0;
+  Field a{}, b{};
+  double alpha = 0.0;
+  const double* p0 = nullptr;
+  double* out0 = nullptr;
+  double* out1 = nullptr;
+  double* out2 = nullptr;
+  double e = 0.0;   // LAP5
+  SHCoef c{};
+  double sc = 1.0;  // FDJVP step
+  double* partial = nullptr;  // TRIAL: [3][nblk]
+};
+
+// Launches one stencil pass.  *nblk receives the number of partial-sum slots written (TRIAL).
+hipError_t stencil_launch(SMode m, const StencilArgs& a, hipStream_t s, int64_t* nblk);
+// Upper bound of the partial-sum slots one stencil pass with reductions (TRIAL) writes.
+int64_t stencil_partial_slots(int64_t ny, int64_t nx);
+// Algorithmic HBM bytes per grid point of one pass (for roofline accounting).
+double stencil_bytes_per_point(SMode m, bool has_xt);
+
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxVec = 64;
+struct VecList {
+  const double* p[kMaxVec];
+  double c[kMaxVec];
+};
+
+constexpr int kKrylovBlock = 256;
+constexpr int kKrylovPerThread = 8;
+constexpr int64_t kKrylovChunk = int64_t(kKrylovBlock) * kKrylovPerThread;
+
+inline int64_t krylov_blocks(int64_t n) { return (n + kKrylovChunk - 1) / kKrylovChunk; }
+
+// partial[(i)*nblk + b]: a.p_i for i < np, g.p_i at np+i (g may be null -> zeros), a.a at 2np.
+hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
+                       double* partial, hipStream_t s, int64_t* nblk);
+// out = cin*in + sum_i c_i p_i (in may be null); partial: [0] sum out^2, [1] max|out|.
+// out may alias `in` or any p_i (element-wise, each element read and written by one thread).
+hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
+                        int64_t n, double* partial, hipStream_t s, int64_t* nblk);
+// result[k] = sum_b partial[k*nblk + b] for k < nsum, NaN-propagating max for nsum <= k < nv.
+hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,
+                               double* result, hipStream_t s);
+// out = a*x + b*y (y may be null; out may alias x or y).  Element-wise helper of the generic
+// residual path (nk_solve) and of nk_axpy / nk_scal.
+// w = (w - f0) / sc, the finite difference of KrylovJacobian.matvec (_nonlin.py:1509).
+hipError_t fddiff_launch(double* w, const double* f0, double sc, int64_t n, hipStream_t s);
+hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
+                        int64_t n, hipStream_t s);
+
+}  // namespace nk

@@ -1,0 +1,582 @@
+// Host-side inexact Newton / LGMRES driver (see nk_solver.h).
+//
+// Algorithm follows SciPy 1.15.3 line by line where it is observable:
+//   nonlin_solve ............ scipy/optimize/_nonlin.py:122-268
+//   _nonlin_line_search ..... scipy/optimize/_nonlin.py:272-314
+//   scalar_search_armijo .... scipy/optimize/_linesearch.py:684-739
+//   TerminationCondition .... scipy/optimize/_nonlin.py:317-375
+//   KrylovJacobian .......... scipy/optimize/_nonlin.py:1453-1540
+//   lgmres (maxiter=1) ...... scipy/sparse/linalg/_isolve/lgmres.py:120-230
+//   _fgmres ................. scipy/sparse/linalg/_isolve/_gcrotmk.py:14-180
+// The C++ twin's solver (`nonlin_solve`, `KrylovJacobian`, `lgmres`, `scalar_search_armijo`,
+// `maxnorm` from newton_krylov.obj) is the same algorithm.
+#include "nk_solver.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace nk {
+
+namespace {
+constexpr double kEps = DBL_EPSILON;
+constexpr int kReduceSlots = 2 * kMaxVec + 8;
+}  // namespace
+
+nk_opts default_opts() {
+  nk_opts o;
+  o.f_tol = NAN;
+  o.f_rtol = NAN;
+  o.x_tol = NAN;
+  o.x_rtol = NAN;
+  o.rdiff = 0.0;
+  o.maxiter = 0;
+  o.inner_m = 30;
+  o.outer_k = 10;
+  o.line_search = 1;
+  o.jvp_mode = NK_JVP_FD;
+  o.verbose = 0;
+  o.profile = 0;
+  return o;
+}
+
+// ============================================================================================
+// Engine
+// ============================================================================================
+Engine::Engine(int64_t n_, nk_comm* comm_, hipStream_t s_, bool profile_, int64_t min_partial)
+    : n(n_), npad(pad(n_)), comm(comm_), s(s_), profile(profile_) {
+  // partial-sum slots: the larger of the Krylov multi-dot and the problem's stencil reductions
+  const int64_t kb = krylov_blocks(npad) + 1;
+  const int64_t cap = std::max<int64_t>((2 * kMaxVec + 1) * kb, min_partial);
+  if (hipMalloc(reinterpret_cast<void**>(&partial_), sizeof(double) * cap) != hipSuccess)
+    partial_ = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&dres_), sizeof(double) * kReduceSlots) != hipSuccess)
+    dres_ = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&hres_), sizeof(double) * kReduceSlots, 0) !=
+      hipSuccess)
+    hres_ = nullptr;
+  bytes_ = sizeof(double) * (cap + kReduceSlots);
+}
+
+Engine::~Engine() {
+  if (s) hipStreamSynchronize(s);
+  for (auto& p : pend_) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : free_ev_) hipEventDestroy(e);
+  if (own_pool_ && pool_) hipFree(pool_);
+  if (partial_) hipFree(partial_);
+  if (dres_) hipFree(dres_);
+  if (hres_) hipHostFree(hres_);
+}
+
+int Engine::alloc(int count, std::vector<double*>* out, void* external, int64_t external_bytes) {
+  if (!partial_ || !dres_ || !hres_) return NK_ENOMEM;
+  const int64_t bytes = sizeof(double) * npad * int64_t(count);
+  if (external) {
+    if (external_bytes < bytes || (reinterpret_cast<uintptr_t>(external) & 255u)) return NK_EINVAL;
+    pool_ = static_cast<double*>(external);
+    own_pool_ = false;
+  } else {
+    if (hipMalloc(reinterpret_cast<void**>(&pool_), bytes) != hipSuccess) {
+      pool_ = nullptr;
+      return NK_ENOMEM;
+    }
+    own_pool_ = true;
+    bytes_ += bytes;
+  }
+  if (hipMemsetAsync(pool_, 0, bytes, s) != hipSuccess) return NK_EHIP;
+  out->resize(count);
+  for (int i = 0; i < count; ++i) (*out)[i] = pool_ + npad * i;
+  return NK_OK;
+}
+
+hipEvent_t Engine::ev() {
+  if (!free_ev_.empty()) {
+    hipEvent_t e = free_ev_.back();
+    free_ev_.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+void Engine::harvest() {
+  for (auto& p : pend_) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    stats_[p.kind].launches += 1;
+    stats_[p.kind].ms += ms;
+    stats_[p.kind].bytes += p.bytes;
+    free_ev_.push_back(p.a);
+    free_ev_.push_back(p.b);
+  }
+  pend_.clear();
+}
+
+void Engine::reset_stats() {
+  for (auto& k : stats_) k = KStat{};
+}
+
+int Engine::sync() {
+  if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+  harvest();
+  return NK_OK;
+}
+
+int Engine::copy(double* dst, const double* src, int64_t cnt) {
+  if (dst == src) return NK_OK;
+  return launch(K_COPY, 16.0 * cnt, [&] {
+    return hipMemcpyAsync(dst, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s);
+  });
+}
+
+int Engine::reduce(int64_t nblk, int nsum, int nv, double* out) {
+  if (nv > kReduceSlots) return NK_EINVAL;
+  int rc = launch(K_REDUCE, 8.0 * nblk * nv,
+                  [&] { return reduce_final_launch(partial_, nblk, nsum, nv, dres_, s); });
+  if (rc) return rc;
+  if (comm && comm->size() > 1) {
+    rc = comm->allreduce(dres_, hres_, nsum, nv, s);
+    if (rc) return rc;
+  } else {
+    if (hipMemcpyAsync(hres_, dres_, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return NK_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+  }
+  harvest();
+  std::memcpy(out, hres_, sizeof(double) * nv);
+  return NK_OK;
+}
+
+// ============================================================================================
+// Newton-Krylov core
+// ============================================================================================
+namespace {
+
+void givens(double a, double b, double* c, double* s) {
+  if (b == 0.0) {
+    *c = 1.0;
+    *s = 0.0;
+    return;
+  }
+  const double r = std::hypot(a, b);
+  *c = a / r;
+  *s = b / r;
+}
+
+// Least-squares solve of the (n x n) upper-triangular R y = g (lstsq in _gcrotmk.py:177):
+// back-substitution when R is well conditioned on its diagonal, otherwise a one-sided Jacobi
+// SVD pseudo-inverse with gelsd's cut-off rcond = eps * n.
+void lstsq_upper(const double (*R)[kMaxVec + 1], int n, const double* g, double* y) {
+  double dmax = 0.0, dmin = INFINITY;
+  for (int i = 0; i < n; ++i) {
+    dmax = std::max(dmax, std::fabs(R[i][i]));
+    dmin = std::min(dmin, std::fabs(R[i][i]));
+  }
+  if (n > 0 && dmin > kEps * n * dmax) {
+    for (int i = n - 1; i >= 0; --i) {
+      double acc = g[i];
+      for (int k = i + 1; k < n; ++k) acc -= R[i][k] * y[k];
+      y[i] = acc / R[i][i];
+    }
+    return;
+  }
+  // A = R (n x n), one-sided Jacobi: A V = U S
+  std::vector<double> A(n * n), Vm(n * n, 0.0);
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < n; ++k) A[i * n + k] = (k >= i) ? R[i][k] : 0.0;
+  for (int i = 0; i < n; ++i) Vm[i * n + i] = 1.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < n - 1; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        double a = 0, b = 0, c = 0;
+        for (int i = 0; i < n; ++i) {
+          a += A[i * n + p] * A[i * n + p];
+          b += A[i * n + q] * A[i * n + q];
+          c += A[i * n + p] * A[i * n + q];
+        }
+        if (c == 0.0) continue;
+        off = std::max(off, std::fabs(c) / std::sqrt(a * b + 1e-300));
+        const double zeta = (b - a) / (2.0 * c);
+        const double t = std::copysign(1.0, zeta) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+        const double cs = 1.0 / std::sqrt(1.0 + t * t), sn = cs * t;
+        for (int i = 0; i < n; ++i) {
+          const double ap = A[i * n + p], aq = A[i * n + q];
+          A[i * n + p] = cs * ap - sn * aq;
+          A[i * n + q] = sn * ap + cs * aq;
+          const double vp = Vm[i * n + p], vq = Vm[i * n + q];
+          Vm[i * n + p] = cs * vp - sn * vq;
+          Vm[i * n + q] = sn * vp + cs * vq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  std::vector<double> sig(n);
+  double smax = 0.0;
+  for (int k = 0; k < n; ++k) {
+    double acc = 0;
+    for (int i = 0; i < n; ++i) acc += A[i * n + k] * A[i * n + k];
+    sig[k] = std::sqrt(acc);
+    smax = std::max(smax, sig[k]);
+  }
+  const double cut = kEps * n * smax;
+  for (int i = 0; i < n; ++i) y[i] = 0.0;
+  for (int k = 0; k < n; ++k) {
+    if (!(sig[k] > cut)) continue;
+    double ug = 0.0;  // u_k . g with u_k = A[:,k] / sig_k
+    for (int i = 0; i < n; ++i) ug += A[i * n + k] * g[i];
+    ug /= sig[k] * sig[k];
+    for (int i = 0; i < n; ++i) y[i] += Vm[i * n + k] * ug;
+  }
+}
+
+}  // namespace
+
+NewtonKrylov::NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* external,
+                           int64_t external_bytes)
+    : E_(E), P_(P), o_(o) {
+  if (o.inner_m < 1 || o.outer_k < 0 || o.inner_m + o.outer_k + 1 > kMaxVec) {
+    init_status_ = NK_EINVAL;
+    return;
+  }
+  std::vector<double*> v;
+  init_status_ = E_.alloc(vectors_needed(o), &v, external, external_bytes);
+  if (init_status_) return;
+  int q = 0;
+  X_ = v[q++];
+  Xt_ = v[q++];
+  Fx_ = v[q++];
+  Ft_ = v[q++];
+  G0_ = v[q++];
+  Gt_ = v[q++];
+  const int nv = o.inner_m + o.outer_k + 1;
+  V_.assign(nv, nullptr);
+  for (int i = 1; i < nv; ++i) V_[i] = v[q++];
+  outer_.assign(std::max(o.outer_k, 1), nullptr);
+  for (int i = 0; i < std::max(o.outer_k, 1); ++i) outer_[i] = v[q++];
+  osig_.assign(outer_.size(), 0.0);
+  orn_.assign(outer_.size(), 0.0);
+}
+
+int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec) {
+  // scipy/sparse/linalg/_isolve/lgmres.py:120-230 with x0 = 0, maxiter = 1, M = identity.
+  *dnorm = 0.0;
+  *dmax = 0.0;
+  *dvec = nullptr;
+  const double b_norm = fx_norm_;
+  if (b_norm == 0.0) return NK_OK;  // x = b = 0  -> zero step
+  const double atol = std::max(0.0, tol * b_norm);
+  const double r_norm = b_norm;  // r_outer = matvec(0) - b = -b (matvec(0) short-circuits)
+  if (r_norm <= std::max(atol, tol * b_norm)) return NK_OK;
+  const double ptol = std::min(1.0, std::max(atol, tol * b_norm) / r_norm);
+
+  const int n_o = ocount_;
+  const int m = o_.inner_m + n_o;
+  const int64_t n = E_.n;
+  V_[0] = Fx_;  // v0 = b / |b|, kept raw with scale 1/|b|
+  double sig[kMaxVec + 1], rn[kMaxVec + 1];
+  sig[0] = 1.0 / b_norm;
+  rn[0] = b_norm;
+  static thread_local double R[kMaxVec + 1][kMaxVec + 1];
+  static thread_local double gram[kMaxVec + 1][kMaxVec + 1];
+  double cs[kMaxVec + 1], sn[kMaxVec + 1], gv[kMaxVec + 2], hcur[kMaxVec + 2], h[kMaxVec + 1];
+  const double* zp[kMaxVec + 1];
+  double zs[kMaxVec + 1];
+  for (int i = 0; i <= m + 1 && i < kMaxVec + 2; ++i) gv[i] = 0.0;
+  gv[0] = 1.0;
+  double red[kReduceSlots];
+  int j = 0;
+  bool breakdown = false;
+  int rc = NK_OK;
+  for (j = 0; j < m; ++j) {
+    // -- Krylov direction z_j (_gcrotmk.py:107-118 with prepend_outer_v=True)
+    const double* z;
+    double zsig, zrn;
+    if (j < n_o) {
+      const int slot = (ohead_ + j) % int(outer_.size());
+      z = outer_[slot];
+      zsig = osig_[slot];
+      zrn = orn_[slot];
+    } else if (j == n_o) {
+      z = V_[0];
+      zsig = sig[0];
+      zrn = rn[0];
+    } else {
+      z = V_[j];
+      zsig = sig[j];
+      zrn = rn[j];
+    }
+    double* w = V_[j + 1];
+    const double nv = zsig * zrn;  // |z|_2 of the normalised vector (KrylovJacobian.matvec :1506)
+    if (nv == 0.0) {
+      rc = E_.launch(K_COPY, 8.0 * n,
+                     [&] { return hipMemsetAsync(w, 0, sizeof(double) * n, E_.s); });
+    } else {
+      const double sc = omega_ / nv;
+      rc = P_.jvp(X_, G0_, z, zsig, sc, w);
+      st_->njvp += 1;
+    }
+    if (rc) return rc;
+    st_->n_arnoldi += 1;
+    // -- one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i < j), |w|^2
+    VecList P;
+    for (int i = 0; i <= j; ++i) P.p[i] = V_[i];
+    int64_t nblk = 0;
+    const double* g = (j > 0) ? V_[j] : nullptr;
+    rc = E_.launch(K_MDOT, 8.0 * n * (j + 2),
+                   [&] { return mdot_launch(w, g, P, j + 1, n, E_.partial(), E_.s, &nblk); });
+    if (rc) return rc;
+    const int np = j + 1;
+    rc = E_.reduce(nblk, 2 * np + 1, 2 * np + 1, red);
+    if (rc) return rc;
+    const double ww = red[2 * np];
+    if (!std::isfinite(ww)) return NK_NONFINITE;  // _nonlin.py:1511-1512
+    const double w_norm = std::sqrt(ww);
+    for (int i = 0; i < j; ++i) gram[j][i] = sig[j] * sig[i] * red[np + i];
+    // MGS coefficients from the Gram matrix: (I + L) h = V^T w (inverse compact WY form)
+    for (int i = 0; i <= j; ++i) {
+      double acc = sig[i] * red[i];
+      for (int k = 0; k < i; ++k) acc -= gram[i][k] * h[k];
+      h[i] = acc;
+    }
+    VecList U;
+    for (int i = 0; i <= j; ++i) {
+      U.p[i] = V_[i];
+      U.c[i] = -h[i] * sig[i];
+    }
+    rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
+      return combo_launch(w, w, 1.0, U, j + 1, n, E_.partial(), E_.s, &nblk);
+    });
+    if (rc) return rc;
+    rc = E_.reduce(nblk, 1, 2, red);
+    if (rc) return rc;
+    const double hn = std::sqrt(red[0]);
+    for (int i = 0; i <= j; ++i) hcur[i] = h[i];
+    hcur[j + 1] = hn;
+    const double alpha = 1.0 / hn;
+    sig[j + 1] = std::isfinite(alpha) ? alpha : 1.0;
+    rn[j + 1] = hn;
+    if (!(hn > kEps * w_norm)) breakdown = true;
+    zp[j] = z;
+    zs[j] = zsig;
+    // -- Givens update of the Hessenberg QR (qr_insert, _gcrotmk.py:146-158)
+    for (int i = 0; i < j; ++i) {
+      const double t = cs[i] * hcur[i] + sn[i] * hcur[i + 1];
+      hcur[i + 1] = -sn[i] * hcur[i] + cs[i] * hcur[i + 1];
+      hcur[i] = t;
+    }
+    givens(hcur[j], hcur[j + 1], &cs[j], &sn[j]);
+    hcur[j] = cs[j] * hcur[j] + sn[j] * hcur[j + 1];
+    for (int i = 0; i <= j; ++i) R[i][j] = hcur[i];
+    gv[j + 1] = -sn[j] * gv[j];
+    gv[j] = cs[j] * gv[j];
+    const double res = std::fabs(gv[j + 1]);
+    if (res < ptol || breakdown) break;
+  }
+  if (j == m) j = m - 1;
+  if (!std::isfinite(R[j][j])) return NK_OK;  // LinAlgError -> lgmres returns x = 0
+  double y[kMaxVec + 1];
+  lstsq_upper(R, j + 1, gv, y);
+  for (int i = 0; i <= j; ++i) {
+    y[i] *= b_norm;  // y *= inner_res_0
+    if (!std::isfinite(y[i])) return NK_OK;
+  }
+  // -- dx = sum_i y_i z_i into the next outer slot (the oldest one if the ring is full; the
+  //    combination reads each element before writing it, so in-place is safe)
+  const int K = int(outer_.size());
+  const int slot = (o_.outer_k > 0 && ocount_ < o_.outer_k) ? (ohead_ + ocount_) % K : ohead_;
+  VecList Z;
+  for (int i = 0; i <= j; ++i) {
+    Z.p[i] = zp[i];
+    Z.c[i] = y[i] * zs[i];
+  }
+  int64_t nblk = 0;
+  double* d = outer_[slot];
+  rc = E_.launch(K_COMBO, 8.0 * n * (j + 2), [&] {
+    return combo_launch(d, nullptr, 0.0, Z, j + 1, n, E_.partial(), E_.s, &nblk);
+  });
+  if (rc) return rc;
+  rc = E_.reduce(nblk, 1, 2, red);
+  if (rc) return rc;
+  const double nx = std::sqrt(red[0]);
+  if (nx > 0 && o_.outer_k > 0) {
+    osig_[slot] = 1.0 / nx;
+    orn_[slot] = nx;
+    if (ocount_ < o_.outer_k)
+      ++ocount_;
+    else
+      ohead_ = (ohead_ + 1) % K;
+  }
+  *dnorm = nx;
+  *dmax = red[1];
+  *dvec = d;
+  return NK_OK;
+}
+
+int NewtonKrylov::line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax) {
+  // _nonlin_line_search(search_type='armijo', smin=1e-2) + scalar_search_armijo(c1=1e-4)
+  double tmp_s = 0.0, tmp_phi = fx_norm_ * fx_norm_;
+  double tmp_fmax = 0.0, tmp_xmax = 0.0, tmp_sum = tmp_phi;
+  int rc = NK_OK;
+  auto phi = [&](double s) -> double {
+    if (s == tmp_s) return tmp_phi;
+    double red[3];
+    rc = P_.eval(X_, d_, -s, Xt_, Ft_, Gt_, red);
+    st_->nfev += 1;
+    const double p = std::isfinite(red[0]) ? red[0] : INFINITY;
+    tmp_s = s;
+    tmp_phi = p;
+    tmp_sum = red[0];
+    tmp_fmax = std::isfinite(red[0]) ? red[1] : NAN;
+    tmp_xmax = red[2];
+    return p;
+  };
+  double s = 1.0;
+  bool found = true;
+  if (o_.line_search) {
+    const double phi0 = tmp_phi, derphi0 = -tmp_phi, c1 = 1e-4, amin = 1e-2;
+    double alpha0 = 1.0;
+    double phi_a0 = phi(alpha0);
+    if (rc) return rc;
+    if (phi_a0 <= phi0 + c1 * alpha0 * derphi0) {
+      s = alpha0;
+    } else {
+      double alpha1 = -(derphi0)*alpha0 * alpha0 / 2.0 / (phi_a0 - phi0 - derphi0 * alpha0);
+      double phi_a1 = phi(alpha1);
+      if (rc) return rc;
+      if (phi_a1 <= phi0 + c1 * alpha1 * derphi0) {
+        s = alpha1;
+      } else {
+        found = false;
+        while (alpha1 > amin) {
+          const double factor = alpha0 * alpha0 * alpha1 * alpha1 * (alpha1 - alpha0);
+          double a = alpha0 * alpha0 * (phi_a1 - phi0 - derphi0 * alpha1) -
+                     alpha1 * alpha1 * (phi_a0 - phi0 - derphi0 * alpha0);
+          a = a / factor;
+          double b = -alpha0 * alpha0 * alpha0 * (phi_a1 - phi0 - derphi0 * alpha1) +
+                     alpha1 * alpha1 * alpha1 * (phi_a0 - phi0 - derphi0 * alpha0);
+          b = b / factor;
+          double alpha2 = (-b + std::sqrt(std::fabs(b * b - 3 * a * derphi0))) / (3.0 * a);
+          const double phi_a2 = phi(alpha2);
+          if (rc) return rc;
+          if (phi_a2 <= phi0 + c1 * alpha2 * derphi0) {
+            s = alpha2;
+            found = true;
+            break;
+          }
+          if ((alpha1 - alpha2) > alpha1 / 2.0 || (1 - alpha2 / alpha1) < 0.96) alpha2 = alpha1 / 2.0;
+          alpha0 = alpha1;
+          alpha1 = alpha2;
+          phi_a0 = phi_a1;
+          phi_a1 = phi_a2;
+        }
+        if (!found) s = 1.0;  // "take the full Newton step and hope for the best"
+      }
+    }
+    if (s != tmp_s) phi(s);  // Fx = func(x) at the accepted step
+    if (rc) return rc;
+  } else {
+    phi(1.0);
+    if (rc) return rc;
+  }
+  *s_out = s;
+  *fnorm_new = std::sqrt(tmp_sum);
+  *fmax = tmp_fmax;
+  *xmax = tmp_xmax;
+  return NK_OK;
+}
+
+int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
+  if (init_status_) return init_status_;
+  nk_stats dummy;
+  st_ = st ? st : &dummy;
+  std::memset(st_, 0, sizeof(nk_stats));
+  ocount_ = 0;
+  ohead_ = 0;
+  const int64_t n = E_.n;
+  const double f_tol = std::isnan(o_.f_tol) ? std::pow(kEps, 1.0 / 3.0) : o_.f_tol;
+  const double f_rtol = std::isnan(o_.f_rtol) ? INFINITY : o_.f_rtol;
+  const double x_tol = std::isnan(o_.x_tol) ? INFINITY : o_.x_tol;
+  const double x_rtol = std::isnan(o_.x_rtol) ? INFINITY : o_.x_rtol;
+  rdiff_ = (o_.rdiff > 0) ? o_.rdiff : std::pow(kEps, 0.5);
+  const int64_t maxiter = (o_.maxiter > 0) ? o_.maxiter : 100 * (P_.n_global() + 1);
+  const bool talk = o_.verbose && (!E_.comm || E_.comm->rank() == 0);
+
+  int rc = E_.copy(X_, x_in, n);
+  if (!rc) rc = P_.set_x0(X_);
+  double red[3];
+  if (!rc) rc = P_.eval(X_, X_, 0.0, nullptr, Fx_, G0_, red);
+  if (rc) return rc;
+  st_->nfev = 1;
+  fx_norm_ = std::sqrt(red[0]);
+  double fmax = std::isfinite(red[0]) ? red[1] : NAN;
+  double xmax = red[2];
+  // KrylovJacobian.setup / _update_diff_step
+  omega_ = rdiff_ * std::max(1.0, xmax) / std::max(1.0, fmax);
+  const double gamma = 0.9, eta_max = 0.9999, eta_treshold = 0.1;
+  double eta = 1e-3;
+  double dxmax = INFINITY;
+  double f0_norm = NAN;
+  bool converged = false;
+  int64_t it = 0;
+  for (it = 0; it < maxiter; ++it) {
+    // TerminationCondition.check (max-norm)
+    const double f_norm = fmax;
+    if (std::isnan(f0_norm)) f0_norm = f_norm;
+    if (f_norm == 0.0 || ((f_norm <= f_tol && f_norm / f_rtol <= f0_norm) &&
+                          (dxmax <= x_tol && dxmax / x_rtol <= xmax))) {
+      converged = true;
+      break;
+    }
+    const double tol = std::min(eta, eta * fx_norm_);
+    double dnorm = 0.0, dmx = 0.0;
+    rc = lgmres(tol, &dnorm, &dmx, &d_);
+    if (rc) break;
+    if (!(dnorm != 0.0) || d_ == nullptr) {
+      rc = NK_ZERO_STEP;
+      break;
+    }
+    dxmax = dmx;
+    rc = P_.set_dir(d_);
+    if (rc) break;
+    double s = 1.0, fnorm_new = 0.0;
+    rc = line_search(&s, &fnorm_new, &fmax, &xmax);
+    if (rc) break;
+    std::swap(X_, Xt_);
+    std::swap(Fx_, Ft_);
+    std::swap(G0_, Gt_);
+    rc = P_.set_x0(X_);
+    if (rc) break;
+    omega_ = rdiff_ * std::max(1.0, xmax) / std::max(1.0, fmax);  // jacobian.update
+    const double eta_A = gamma * fnorm_new * fnorm_new / (fx_norm_ * fx_norm_);
+    if (gamma * eta * eta < eta_treshold)
+      eta = std::min(eta_max, eta_A);
+    else
+      eta = std::min(eta_max, std::max(eta_A, gamma * eta * eta));
+    fx_norm_ = fnorm_new;
+    if (talk) {
+      std::printf("%lld:  |F(x)| = %g; step %g\n", static_cast<long long>(it), fmax, s);
+      std::fflush(stdout);
+    }
+  }
+  st_->nit = it;
+  st_->fnorm_inf = fmax;
+  st_->fnorm_2 = fx_norm_;
+  if (rc) {
+    st_->status = rc;
+    return rc;
+  }
+  rc = E_.copy(x_out, X_, n);
+  if (!rc) rc = E_.sync();
+  if (rc) return rc;
+  st_->status = converged ? NK_OK : NK_NO_CONVERGENCE;
+  return st_->status;
+}
+
+}  // namespace nk

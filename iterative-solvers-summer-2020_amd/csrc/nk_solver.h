@@ -1,0 +1,169 @@
+// Host-side inexact Newton / LGMRES driver of libnkhip.
+//
+// A C++ restatement of SciPy 1.15.3's newton_krylov stack as the reference calls it
+// (sh_scipy_nk.py:61 `newton_krylov(residual, Uo)`; the C++ twin's external `nonlin_solve`,
+// main.cpp:104), re-designed for one GPU stream per rank:
+//   * every N^2-sized vector lives in HBM; the host only holds scalars and the <= 64x64
+//     Hessenberg factorisation;
+//   * per Arnoldi step: one JVP kernel, one fused multi-dot (V^T w, new Gram row, |w|^2),
+//     one fused update (w - V h, |w'|^2) -- the MGS coefficients are recovered from the Gram
+//     row (inverse compact-WY MGS), which equals scipy's MGS in exact arithmetic;
+//   * basis vectors are kept un-normalised with a host-side scale (no scal pass).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/nkhip.h"
+#include "comm.h"
+#include "nk_kernels.h"
+
+namespace nk {
+
+enum Kind : int {
+  K_FDJVP = 0,
+  K_AJVP,
+  K_TRIAL,
+  K_BOLD,
+  K_MDOT,
+  K_COMBO,
+  K_REDUCE,
+  K_COPY,
+  K_HALO,
+  K_USERF,
+  K_AXPBY,
+  K_NKINDS
+};
+
+struct KStat {
+  int64_t launches = 0;
+  double ms = 0.0;
+  double bytes = 0.0;
+};
+
+// Device workspace, reductions and per-kernel profiling for one rank's solver.
+class Engine {
+ public:
+  // min_partial: partial-sum slots any kernel of the problem needs beyond the Krylov ones.
+  Engine(int64_t n, nk_comm* comm, hipStream_t s, bool profile, int64_t min_partial = 0);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  // Allocate `count` zeroed vectors of npad doubles from one pool (or carve from `external`).
+  int alloc(int count, std::vector<double*>* out, void* external = nullptr,
+            int64_t external_bytes = 0);
+  static int64_t pad(int64_t n) { return (n + 255) / 256 * 256; }
+
+  template <class L>
+  int launch(int kind, double bytes, L&& fn);
+  // Finish a reduction whose per-block partials are in partial(): values [0,nsum) summed,
+  // [nsum,nv) max-reduced, across blocks and ranks; result in out[0,nv).  Synchronises.
+  int reduce(int64_t nblk, int nsum, int nv, double* out);
+  int sync();
+  int copy(double* dst, const double* src, int64_t n);
+
+  double* partial() const { return partial_; }
+  const KStat& stat(int k) const { return stats_[k]; }
+  void reset_stats();
+  int64_t bytes_allocated() const { return bytes_; }
+
+  int64_t n;
+  int64_t npad;
+  nk_comm* comm;
+  hipStream_t s;
+  bool profile;
+
+ private:
+  void harvest();
+  hipEvent_t ev();
+  double* pool_ = nullptr;
+  bool own_pool_ = false;
+  double* partial_ = nullptr;
+  double* dres_ = nullptr;
+  double* hres_ = nullptr;
+  int64_t bytes_ = 0;
+  struct Pending {
+    int kind;
+    hipEvent_t a, b;
+    double bytes;
+  };
+  std::vector<Pending> pend_;
+  std::vector<hipEvent_t> free_ev_;
+  KStat stats_[K_NKINDS];
+};
+
+template <class L>
+int Engine::launch(int kind, double bytes, L&& fn) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (profile) {
+    a = ev();
+    hipEventRecord(a, s);
+  }
+  const hipError_t e = fn();
+  if (profile) {
+    b = ev();
+    hipEventRecord(b, s);
+    pend_.push_back(Pending{kind, a, b, bytes});
+  } else {
+    stats_[kind].launches += 1;
+    stats_[kind].bytes += bytes;
+  }
+  return e == hipSuccess ? NK_OK : NK_EHIP;
+}
+
+// The nonlinear problem seen by the Newton-Krylov core.
+struct Problem {
+  virtual ~Problem() = default;
+  virtual int64_t n_global() const = 0;
+  // F(x + alpha p) -> F; G = the x-dependent part that the FD JVP differences (F = G + const);
+  // xt = x + alpha p if non-null.  red = {sum F^2, max|F|, max|x + alpha p|} over all ranks.
+  virtual int eval(const double* x, const double* p, double alpha, double* xt, double* F,
+                   double* G, double red[3]) = 0;
+  // w = J z.  FD: w = (G(x0 + sc*zs*z) - G0)/sc (KrylovJacobian.matvec); analytic: zs*J(x0) z.
+  virtual int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
+                  double* w) = 0;
+  virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
+  virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
+};
+
+// nonlin_solve + KrylovJacobian + lgmres(maxiter=1, outer_k, prepend_outer_v) on one Problem.
+class NewtonKrylov {
+ public:
+  NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* external = nullptr,
+               int64_t external_bytes = 0);
+  int status() const { return init_status_; }
+  void set_opts(const nk_opts& o) { o_ = o; }
+  // x_out = root of F starting from x_in (device, length n; may alias).  Returns NK_* status.
+  int solve(const double* x_in, double* x_out, nk_stats* st);
+  static int vectors_needed(const nk_opts& o) { return o.inner_m + 2 * o.outer_k + 8; }
+
+ private:
+  int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
+  int line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax);
+
+  Engine& E_;
+  Problem& P_;
+  nk_opts o_;
+  int init_status_ = NK_OK;
+  // vectors
+  double *X_ = nullptr, *Xt_ = nullptr, *Fx_ = nullptr, *Ft_ = nullptr, *G0_ = nullptr,
+         *Gt_ = nullptr;
+  std::vector<double*> V_;      // V_[0] aliases Fx_ during a solve
+  std::vector<double*> outer_;  // LGMRES augmentation ring
+  std::vector<double> osig_, orn_;
+  int ocount_ = 0, ohead_ = 0;
+  double omega_ = 0.0;
+  double* d_ = nullptr;  // current search direction (an outer slot)
+  nk_stats* st_ = nullptr;
+  double fx_norm_ = 0.0;
+  double rdiff_ = 0.0;
+};
+
+// Default options (SciPy newton_krylov defaults).
+nk_opts default_opts();
+
+}  // namespace nk

@@ -1,0 +1,63 @@
+// Problems handed to the Newton-Krylov core: the fused Swift-Hohenberg stepper (north-star path)
+// and a generic device residual supplied through a C callback (the newton_krylov drop-in).
+#pragma once
+
+#include "nk_solver.h"
+
+namespace nk {
+
+// Crank-Nicolson Swift-Hohenberg residual on one row slab (sh_scipy_nk.py:47-49 / main.cpp:19-32),
+// F(u) = G(u) + B with G(u) = u/k - (L u + g u^2 - u^3)/2 and B = -Uo/k - (L Uo + g Uo^2 - Uo^3)/2
+// hoisted once per time step (the reference recomputes L@Uo on every call).
+class SHProblem final : public Problem {
+ public:
+  SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoef c, int jvp_mode);
+  ~SHProblem() override;
+  int status() const { return status_; }
+  void set_jvp_mode(int m) { jvp_mode_ = m; }
+  int64_t n_global() const override { return ny_g_ * nx_; }
+  int prepare(const double* u_prev);  // B <- B(u_prev)
+  int eval(const double* x, const double* p, double alpha, double* xt, double* F, double* G,
+           double red[3]) override;
+  int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
+          double* w) override;
+  int set_x0(const double* x0) override;
+  int set_dir(const double* d) override;
+
+ private:
+  bool dist() const { return E_.comm && E_.comm->size() > 1; }
+  Field field(const double* p, const double* halo) const;
+  int halo(const double* v, double* h);
+  Engine& E_;
+  int64_t ny_, nx_, ny_g_;
+  SHCoef c_;
+  int jvp_mode_;
+  int status_ = NK_OK;
+  double* B_ = nullptr;
+  double* hx_ = nullptr;  // halos (4 rows each: lo = rows -2,-1 ; hi = rows ny, ny+1)
+  double* hz_ = nullptr;
+  double* hd_ = nullptr;
+  double* hu_ = nullptr;
+};
+
+// newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):
+// the FD Jacobian of KrylovJacobian.matvec built from F evaluations.
+class CallbackProblem final : public Problem {
+ public:
+  CallbackProblem(Engine& E, nk_residual_fn F, void* ctx, double* tmp, double* tmp2);
+  int64_t n_global() const override { return E_.n; }
+  int eval(const double* x, const double* p, double alpha, double* xt, double* F, double* G,
+           double red[3]) override;
+  int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
+          double* w) override;
+
+ private:
+  int norms(double* v, double* sum2, double* vmax);
+  Engine& E_;
+  nk_residual_fn F_;
+  void* ctx_;
+  double* tmp_;
+  double* tmp2_;
+};
+
+}  // namespace nk

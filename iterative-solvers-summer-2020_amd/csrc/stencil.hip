@@ -1,0 +1,337 @@
+// Matrix-free stencil kernels of the Swift-Hohenberg Crank-Nicolson residual (gfx950).
+//
+// Replaces the scipy CSR SpMVs `Lap @ v` / `L @ u` and the NumPy element-wise passes of
+// residual() (sh_scipy_nk.py:32-49) and the Eigen SpMV of the C++ twin (main.cpp:19-32):
+// no matrix is stored, the 13 coefficients are closed-form (nk::sh_coef).
+//
+// Fast path ("march"): a thread owns two adjacent columns (one 16-B double2 per row and field),
+// a block owns 2*BX columns x RY rows and marches down its rows keeping a 5-row register window
+// (3 rows for the 5-point Laplacian).  Each input row enters the window with three coalesced
+// double2 loads (columns c-2.., c.., c+2..); the side loads are L1/L2 hits shared with the
+// neighbouring lanes, so HBM sees each input byte once per block plus the 2*R halo rows.
+// The next row is prefetched one iteration ahead.  Requires nx even and 16-B aligned rows.
+// Generic path ("point"): one output per thread with modular indexing (odd nx, e.g. 61x61).
+#include <cmath>
+
+#include "nk_device.h"
+#include "nk_kernels.h"
+
+namespace nk {
+
+SHCoef sh_coef(double h, double r, double k, double g) {
+  const double e = 1.0 / (h * h);
+  SHCoef c;
+  c.c0 = -20.0 * e * e + 8.0 * e + r - 1.0;
+  c.c1 = 8.0 * e * e - 2.0 * e;
+  c.c2 = -2.0 * e * e;
+  c.c3 = -e * e;
+  c.k = k;
+  c.g = g;
+  return c;
+}
+
+namespace {
+
+struct Nb {
+  double c, a1, dg, a2;  // centre, axial +-1 sum, diagonal sum, axial +-2 sum
+};
+
+struct Res {
+  double o0, o1, o2;
+};
+
+__device__ __forceinline__ const double* rowp(const Field& f, int64_t r, int64_t ny, int64_t nx) {
+  if (r >= 0 && r < ny) return f.base + r * nx;
+  if (f.lo == nullptr) {
+    r %= ny;
+    if (r < 0) r += ny;
+    return f.base + r * nx;
+  }
+  return (r < 0) ? f.lo + (r + 2) * nx : f.hi + (r - ny) * nx;
+}
+
+__device__ __forceinline__ double applyL(const SHCoef& k, const Nb& n) {
+  return k.c0 * n.c + k.c1 * n.a1 + k.c2 * n.dg + k.c3 * n.a2;
+}
+
+// G(w) = w/k - (L w + g w^2 - w^3)/2, so that F(u) = G(u) + B(uo) (sh_scipy_nk.py:49).
+__device__ __forceinline__ double Gfun(const SHCoef& k, double w, double Lw) {
+  const double ww = w * w;
+  return w / k.k - (Lw + k.g * ww - w * ww) / 2;
+}
+
+template <SMode M>
+__device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const Nb& nb, double pv) {
+  Res r{0.0, 0.0, 0.0};
+  const SHCoef& k = A.c;
+  if constexpr (M == SMode::LAP5) {
+    r.o0 = A.e * (na.a1 - 4.0 * na.c);
+  } else if constexpr (M == SMode::SH13) {
+    r.o0 = applyL(k, na);
+  } else if constexpr (M == SMode::RESID) {
+    const double u = na.c, uo = nb.c;
+    const double uu = u * u, uouo = uo * uo;
+    r.o0 = (u - uo) / k.k -
+           (applyL(k, na) + k.g * uu - u * uu + applyL(k, nb) + k.g * uouo - uo * uouo) / 2;
+  } else if constexpr (M == SMode::BOLD) {
+    const double uo = na.c;
+    const double uouo = uo * uo;
+    r.o0 = -uo / k.k - (applyL(k, na) + k.g * uouo - uo * uouo) / 2;
+  } else if constexpr (M == SMode::TRIAL) {
+    const double G = Gfun(k, na.c, applyL(k, na));
+    r.o0 = G + pv;
+    r.o1 = G;
+    r.o2 = na.c;
+  } else if constexpr (M == SMode::FDJVP) {
+    r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) / A.sc;
+  } else {  // AJVP
+    const double z = na.c, u = pv;
+    r.o0 = A.alpha * (z / k.k - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
+  }
+  return r;
+}
+
+template <SMode M>
+constexpr bool kComb = (M == SMode::TRIAL || M == SMode::FDJVP);
+template <SMode M>
+constexpr bool kTwo = (M == SMode::RESID);
+template <SMode M>
+constexpr bool kHasP0 = (M == SMode::TRIAL || M == SMode::FDJVP || M == SMode::AJVP);
+template <SMode M>
+constexpr int kRad = (M == SMode::LAP5) ? 1 : 2;
+
+// ------------------------------------------------------------------------------------------
+// march kernel
+// ------------------------------------------------------------------------------------------
+template <SMode M, int BX>
+__global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
+  constexpr int R = kRad<M>;
+  constexpr int NR = 2 * R + 1;
+  constexpr int NB = kTwo<M> ? NR : 1;
+  const int64_t nx = A.nx, ny = A.ny;
+  const int64_t c0 = 2 * (int64_t(blockIdx.x) * BX + threadIdx.x);
+  const bool active = c0 < nx;
+  const int64_t cc = active ? c0 : 0;
+  const int64_t cm = (cc >= 2) ? cc - 2 : cc - 2 + nx;
+  const int64_t cp = (cc + 2 < nx) ? cc + 2 : cc + 2 - nx;
+
+  auto ld = [&](const Field& f, int64_t r, double (&v)[6]) {
+    const double* p = rowp(f, r, ny, nx);
+    const double2 x0 = *reinterpret_cast<const double2*>(p + cm);
+    const double2 x1 = *reinterpret_cast<const double2*>(p + cc);
+    const double2 x2 = *reinterpret_cast<const double2*>(p + cp);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x1.x; v[3] = x1.y; v[4] = x2.x; v[5] = x2.y;
+  };
+  auto ldw = [&](int64_t r, double (&va)[6], double (&vb)[6]) {
+    ld(A.a, r, va);
+    if constexpr (kComb<M>) {
+      double t[6];
+      ld(A.b, r, t);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) va[q] = va[q] + A.alpha * t[q];
+    } else if constexpr (kTwo<M>) {
+      ld(A.b, r, vb);
+    }
+  };
+
+  double wa[NR][6], wb[NB][6];
+  double na_[6], nb_[6];
+  const int64_t r0 = int64_t(blockIdx.y) * RY;
+  const int64_t r1 = (r0 + RY < ny) ? r0 + RY : ny;
+#pragma unroll
+  for (int m = 0; m < NR; ++m) ldw(r0 - R + m, wa[m], wb[kTwo<M> ? m : 0]);
+
+  double red[3] = {0.0, 0.0, 0.0};
+  for (int64_t r = r0; r < r1; ++r) {
+    if (r + 1 < r1) ldw(r + R + 1, na_, nb_);  // prefetch the next entering row
+    const int64_t o = r * nx + cc;
+    double2 pv = make_double2(0.0, 0.0);
+    if constexpr (kHasP0<M>) {
+      if (active) pv = *reinterpret_cast<const double2*>(A.p0 + o);
+    }
+    Res res[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      Nb a, b{0.0, 0.0, 0.0, 0.0};
+      if constexpr (R == 2) {
+        a.c = wa[2][2 + q];
+        a.a1 = wa[2][1 + q] + wa[2][3 + q] + wa[1][2 + q] + wa[3][2 + q];
+        a.dg = wa[1][1 + q] + wa[1][3 + q] + wa[3][1 + q] + wa[3][3 + q];
+        a.a2 = wa[2][q] + wa[2][4 + q] + wa[0][2 + q] + wa[4][2 + q];
+        if constexpr (kTwo<M>) {
+          b.c = wb[2][2 + q];
+          b.a1 = wb[2][1 + q] + wb[2][3 + q] + wb[1][2 + q] + wb[3][2 + q];
+          b.dg = wb[1][1 + q] + wb[1][3 + q] + wb[3][1 + q] + wb[3][3 + q];
+          b.a2 = wb[2][q] + wb[2][4 + q] + wb[0][2 + q] + wb[4][2 + q];
+        }
+      } else {
+        a.c = wa[1][2 + q];
+        a.a1 = wa[1][1 + q] + wa[1][3 + q] + wa[0][2 + q] + wa[2][2 + q];
+        a.dg = 0.0;
+        a.a2 = 0.0;
+      }
+      res[q] = finish<M>(A, a, b, q == 0 ? pv.x : pv.y);
+    }
+    if (active) {
+      *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
+      if constexpr (M == SMode::TRIAL) {
+        *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
+        if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          red[0] += res[q].o0 * res[q].o0;
+          red[1] = nmax(red[1], fabs(res[q].o0));
+          red[2] = nmax(red[2], fabs(res[q].o2));
+        }
+      }
+    }
+    // shift the window up by one row
+#pragma unroll
+    for (int m = 0; m < NR - 1; ++m) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        wa[m][q] = wa[m + 1][q];
+        if constexpr (kTwo<M>) wb[m][q] = wb[m + 1][q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      wa[NR - 1][q] = na_[q];
+      if constexpr (kTwo<M>) wb[NR - 1][q] = nb_[q];
+    }
+  }
+  if constexpr (M == SMode::TRIAL) {
+    const double v = block_reduce<3, 1, BX>(red);
+    const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
+    const int64_t bid = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
+    if (threadIdx.x < 3) A.partial[threadIdx.x * nblk + bid] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// generic point kernel (any nx, any alignment)
+// ------------------------------------------------------------------------------------------
+template <SMode M>
+__global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
+  constexpr int R = kRad<M>;
+  const int64_t nx = A.nx, ny = A.ny;
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const bool active = idx < nx * ny;
+  double red[3] = {0.0, 0.0, 0.0};
+  if (active) {
+    const int64_t i = idx / nx, j = idx % nx;
+    auto col = [&](int64_t dj) {
+      int64_t c = (j + dj) % nx;
+      if (c < 0) c += nx;
+      return c;
+    };
+    auto val = [&](const Field& f, int64_t di, int64_t dj) {
+      return rowp(f, i + di, ny, nx)[col(dj)];
+    };
+    auto wv = [&](int64_t di, int64_t dj) {
+      double v = val(A.a, di, dj);
+      if constexpr (kComb<M>) v = v + A.alpha * val(A.b, di, dj);
+      return v;
+    };
+    Nb a, b{0.0, 0.0, 0.0, 0.0};
+    a.c = wv(0, 0);
+    a.a1 = wv(0, -1) + wv(0, 1) + wv(-1, 0) + wv(1, 0);
+    if constexpr (R == 2) {
+      a.dg = wv(-1, -1) + wv(-1, 1) + wv(1, -1) + wv(1, 1);
+      a.a2 = wv(0, -2) + wv(0, 2) + wv(-2, 0) + wv(2, 0);
+    } else {
+      a.dg = 0.0;
+      a.a2 = 0.0;
+    }
+    if constexpr (kTwo<M>) {
+      b.c = val(A.b, 0, 0);
+      b.a1 = val(A.b, 0, -1) + val(A.b, 0, 1) + val(A.b, -1, 0) + val(A.b, 1, 0);
+      b.dg = val(A.b, -1, -1) + val(A.b, -1, 1) + val(A.b, 1, -1) + val(A.b, 1, 1);
+      b.a2 = val(A.b, 0, -2) + val(A.b, 0, 2) + val(A.b, -2, 0) + val(A.b, 2, 0);
+    }
+    double pv = 0.0;
+    if constexpr (kHasP0<M>) pv = A.p0[idx];
+    const Res res = finish<M>(A, a, b, pv);
+    A.out0[idx] = res.o0;
+    if constexpr (M == SMode::TRIAL) {
+      A.out1[idx] = res.o1;
+      if (A.out2) A.out2[idx] = res.o2;
+      red[0] = res.o0 * res.o0;
+      red[1] = fabs(res.o0);
+      red[2] = fabs(res.o2);
+    }
+  }
+  if constexpr (M == SMode::TRIAL) {
+    const double v = block_reduce<3, 1, 256>(red);
+    if (threadIdx.x < 3) A.partial[threadIdx.x * int64_t(gridDim.x) + blockIdx.x] = v;
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+bool field_ok(const Field& f) {
+  return f.base == nullptr ||
+         (aligned16(f.base) && (f.lo == nullptr || (aligned16(f.lo) && aligned16(f.hi))));
+}
+
+template <SMode M>
+hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
+  const bool fast = (A.nx % 2 == 0) && A.nx >= 2 && A.ny >= 1 && field_ok(A.a) && field_ok(A.b) &&
+                    aligned16(A.p0) && aligned16(A.out0) && aligned16(A.out1) && aligned16(A.out2);
+  if (fast) {
+    // Row band per block: aim for >= ~2048 blocks (8 per CU) with bands of 4..32 rows.
+    constexpr int BX = 128;
+    const int64_t gx = (A.nx / 2 + BX - 1) / BX;
+    int64_t ry = (A.ny * gx) / 2048;
+    int RY = 4;
+    while (RY < 32 && RY * 2 <= ry) RY *= 2;
+    const int64_t gy = (A.ny + RY - 1) / RY;
+    if (gy > 65535) return hipErrorInvalidValue;
+    if (nblk) *nblk = gx * gy;
+    hipLaunchKernelGGL((march_kernel<M, BX>), dim3(unsigned(gx), unsigned(gy)), dim3(BX), 0, s, A,
+                       RY);
+  } else {
+    const int64_t n = A.nx * A.ny;
+    const int64_t g = (n + 255) / 256;
+    if (nblk) *nblk = g;
+    hipLaunchKernelGGL((point_kernel<M>), dim3(unsigned(g)), dim3(256), 0, s, A);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t stencil_launch(SMode m, const StencilArgs& a, hipStream_t s, int64_t* nblk) {
+  if (a.nx <= 0 || a.ny <= 0) return hipSuccess;
+  switch (m) {
+    case SMode::LAP5: return launch_mode<SMode::LAP5>(a, s, nblk);
+    case SMode::SH13: return launch_mode<SMode::SH13>(a, s, nblk);
+    case SMode::RESID: return launch_mode<SMode::RESID>(a, s, nblk);
+    case SMode::BOLD: return launch_mode<SMode::BOLD>(a, s, nblk);
+    case SMode::TRIAL: return launch_mode<SMode::TRIAL>(a, s, nblk);
+    case SMode::FDJVP: return launch_mode<SMode::FDJVP>(a, s, nblk);
+    case SMode::AJVP: return launch_mode<SMode::AJVP>(a, s, nblk);
+  }
+  return hipErrorInvalidValue;
+}
+
+int64_t stencil_partial_slots(int64_t ny, int64_t nx) {
+  const int64_t march = ((nx / 2 + 127) / 128) * ((ny + 3) / 4);  // RY >= 4, BX = 128
+  const int64_t point = (nx * ny + 255) / 256;
+  return 3 * (march > point ? march : point) + 3;
+}
+
+double stencil_bytes_per_point(SMode m, bool has_xt) {
+  switch (m) {
+    case SMode::LAP5: return 16.0;   // read v, write y
+    case SMode::SH13: return 16.0;
+    case SMode::RESID: return 24.0;  // read u, uo, write F
+    case SMode::BOLD: return 16.0;
+    case SMode::TRIAL: return has_xt ? 48.0 : 40.0;  // read x, d, B; write F, G (, xt)
+    case SMode::FDJVP: return 32.0;  // read x0, z, G0; write Jz
+    case SMode::AJVP: return 24.0;   // read u, z; write Jz
+  }
+  return 0.0;
+}
+
+}  // namespace nk

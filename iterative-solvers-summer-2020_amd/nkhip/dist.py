@@ -1,0 +1,80 @@
+"""Row-slab decomposition of the periodic grid over GPUs (RCCL over xGMI).
+
+The reference is single-process (no MPI/NCCL/Gloo anywhere).  Here the
+N x N torus is cut into row slabs, one per rank (one process per GPU):
+
+* rank p owns rows [row0(p), row0(p) + ny(p)); x stays periodic inside the slab;
+* every stencil pass reads a 2-row halo from the up/down ring neighbours (grouped
+  ncclSend/ncclRecv issued by libnkhip on the solver's stream);
+* dots, norms and max-norms of the Newton-Krylov loop are all-reduced (sum / max) once per
+  fused reduction, so every rank runs the identical host-side Hessenberg algebra.
+
+``slab_rows`` is plain arithmetic (tested on CPU); ``RcclComm.from_torch_distributed`` shares
+the RCCL unique id through an initialised ``torch.distributed`` process group (gloo or nccl).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._lib import check, lib
+
+
+def slab_rows(ny_global: int, rank: int, nranks: int):
+    """(row0, ny_local) of rank's slab: balanced, every slab >= 2 rows (the halo depth)."""
+    if nranks < 1 or not 0 <= rank < nranks:
+        raise ValueError("bad rank / nranks")
+    base, extra = divmod(int(ny_global), int(nranks))
+    ny = base + (1 if rank < extra else 0)
+    row0 = rank * base + min(rank, extra)
+    if nranks > 1 and ny < 2:
+        raise ValueError(f"{ny_global} rows cannot give {nranks} slabs of >= 2 rows")
+    return row0, ny
+
+
+def neighbours(rank: int, nranks: int):
+    """(prev, next) ranks on the periodic ring: prev owns the rows above, next the rows below."""
+    return (rank - 1) % nranks, (rank + 1) % nranks
+
+
+class Comm:
+    def __init__(self, handle, rank, size):
+        self.handle = handle
+        self.rank = rank
+        self.size = size
+
+    def close(self):
+        if self.handle:
+            lib.nk_comm_destroy(self.handle)
+            self.handle = None
+
+
+class RcclComm(Comm):
+    @staticmethod
+    def unique_id() -> bytes:
+        n = lib.nk_comm_unique_id_bytes()
+        buf = (C.c_char * n)()
+        check(lib.nk_comm_get_unique_id(buf), "nk_comm_get_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def create(cls, uid: bytes, rank: int, nranks: int) -> "RcclComm":
+        h = C.c_void_p()
+        buf = (C.c_char * len(uid)).from_buffer_copy(uid)
+        check(lib.nk_comm_create_rccl(C.byref(h), buf, int(rank), int(nranks)),
+              "nk_comm_create_rccl")
+        return cls(h, rank, nranks)
+
+    @classmethod
+    def from_torch_distributed(cls) -> "RcclComm":
+        import torch.distributed as dist
+        rank, size = dist.get_rank(), dist.get_world_size()
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls.create(obj[0], rank, size)
+
+
+def loopback_comms(nranks: int):
+    """``nranks`` slabs on the current GPU, each to be stepped from its own host thread."""
+    arr = (C.c_void_p * nranks)()
+    check(lib.nk_comm_create_loopback(arr, int(nranks)), "nk_comm_create_loopback")
+    return [Comm(C.c_void_p(arr[i]), i, nranks) for i in range(nranks)]

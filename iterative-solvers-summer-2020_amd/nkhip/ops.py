@@ -1,0 +1,141 @@
+"""Device operators over PyTorch-ROCm fp64 tensors, each one call into libnkhip.
+
+These replace the pieces of ``python_work/sh_scipy_nk.py`` one by one:
+``lap5_apply`` = ``Lap @ v`` (:32-35), ``sh13_apply`` = ``L @ v`` (:38-39), ``sh_residual`` =
+``residual(u)`` (:47-49), and the BLAS-1 calls SciPy's Arnoldi makes
+(scipy/sparse/linalg/_isolve/_gcrotmk.py:104-143).  Tensors must be CUDA (HIP) float64; the
+kernels run on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import check, lib
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.float64:
+        raise TypeError(f"{name} must be float64 (the reference computes in fp64)")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+def _ptr(t: torch.Tensor):
+    return C.c_void_p(t.data_ptr())
+
+
+def _grid(v: torch.Tensor, ny, nx):
+    if ny is None or nx is None:
+        if v.dim() != 2:
+            raise ValueError("pass a 2-D (ny, nx) grid or ny/nx explicitly")
+        ny, nx = v.shape
+    if v.numel() != ny * nx:
+        raise ValueError(f"grid {ny}x{nx} does not match {v.numel()} values")
+    return int(ny), int(nx)
+
+
+def lap5_apply(v, e, ny=None, nx=None, out=None):
+    """``Lap @ v``: periodic 5-point Laplacian with e = 1/h^2 (sh_scipy_nk.py:32-35)."""
+    _dev(v, "v")
+    ny, nx = _grid(v, ny, nx)
+    out = torch.empty_like(v) if out is None else _dev(out, "out")
+    check(lib.nk_lap5_apply(_ptr(v), _ptr(out), ny, nx, float(e), _stream()), "nk_lap5_apply")
+    return out
+
+
+def sh13_apply(v, h, r, ny=None, nx=None, out=None):
+    """``L @ v`` with L = -Lap*Lap - 2*Lap + (r-1)*I (sh_scipy_nk.py:38-39)."""
+    _dev(v, "v")
+    ny, nx = _grid(v, ny, nx)
+    out = torch.empty_like(v) if out is None else _dev(out, "out")
+    check(lib.nk_sh13_apply(_ptr(v), _ptr(out), ny, nx, float(h), float(r), _stream()),
+          "nk_sh13_apply")
+    return out
+
+
+def sh_residual(u, uo, h, r, k, g, ny=None, nx=None, out=None):
+    """``residual(u)`` of sh_scipy_nk.py:47-49 with ``Uo = uo``, fused into one pass."""
+    _dev(u, "u")
+    _dev(uo, "uo")
+    ny, nx = _grid(u, ny, nx)
+    out = torch.empty_like(u) if out is None else _dev(out, "out")
+    check(lib.nk_sh_residual(_ptr(u), _ptr(uo), _ptr(out), ny, nx, float(h), float(r), float(k),
+                             float(g), _stream()), "nk_sh_residual")
+    return out
+
+
+def sh_jvp(u, v, h, r, k, g, ny=None, nx=None, out=None):
+    """Exact J(u) v = v/k - (L v + (2 g u - 3 u^2) v)/2 of the residual above."""
+    _dev(u, "u")
+    _dev(v, "v")
+    ny, nx = _grid(u, ny, nx)
+    out = torch.empty_like(u) if out is None else _dev(out, "out")
+    check(lib.nk_sh_jvp(_ptr(u), _ptr(v), _ptr(out), ny, nx, float(h), float(r), float(k),
+                        float(g), _stream()), "nk_sh_jvp")
+    return out
+
+
+def dot(x, y) -> float:
+    _dev(x, "x")
+    _dev(y, "y")
+    r = C.c_double()
+    check(lib.nk_dot(_ptr(x), _ptr(y), x.numel(), C.byref(r), _stream()), "nk_dot")
+    return r.value
+
+
+def nrm2(x) -> float:
+    _dev(x, "x")
+    r = C.c_double()
+    check(lib.nk_nrm2(_ptr(x), x.numel(), C.byref(r), _stream()), "nk_nrm2")
+    return r.value
+
+
+def maxnorm(x) -> float:
+    """``np.absolute(x).max()`` (scipy/optimize/_nonlin.py:36-37)."""
+    _dev(x, "x")
+    r = C.c_double()
+    check(lib.nk_maxnorm(_ptr(x), x.numel(), C.byref(r), _stream()), "nk_maxnorm")
+    return r.value
+
+
+def axpy(a, x, y):
+    """y += a*x in place."""
+    _dev(x, "x")
+    _dev(y, "y")
+    check(lib.nk_axpy(float(a), _ptr(x), _ptr(y), x.numel(), _stream()), "nk_axpy")
+    return y
+
+
+def scal(a, x):
+    _dev(x, "x")
+    check(lib.nk_scal(float(a), _ptr(x), x.numel(), _stream()), "nk_scal")
+    return x
+
+
+def mdot(V, w):
+    """[v . w for v in V] in one pass over w."""
+    _dev(w, "w")
+    m = len(V)
+    ptrs = (C.c_void_p * max(m, 1))(*[_dev(v, "V[i]").data_ptr() for v in V])
+    out = (C.c_double * max(m, 1))()
+    check(lib.nk_mdot(ptrs, m, _ptr(w), w.numel(), out, _stream()), "nk_mdot")
+    return [out[i] for i in range(m)]
+
+
+def maxpy(V, coef, y):
+    """y += sum_i coef[i] * V[i] in one pass."""
+    _dev(y, "y")
+    m = len(V)
+    ptrs = (C.c_void_p * max(m, 1))(*[_dev(v, "V[i]").data_ptr() for v in V])
+    cs = (C.c_double * max(m, 1))(*[float(c) for c in coef])
+    check(lib.nk_maxpy(ptrs, cs, m, _ptr(y), y.numel(), _stream()), "nk_maxpy")
+    return y

@@ -1,0 +1,86 @@
+"""CPU: pin the oracle (NumPy restatement) against the reference's own golden vectors.
+
+The fixtures were produced by executing the reference ``sh_scipy_nk.py`` prologue (lines 1-49)
+and driving ``scipy.optimize.newton_krylov`` as its loop does (tests/golden/make_golden.py).
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import nk_oracle, sh_oracle
+
+OPS = ["ops_n5_d2", "ops_n61", "ops_n64", "ops_n128_h0625"]
+
+
+@pytest.mark.parametrize("name", OPS)
+def test_stencils_match_reference_csr(name):
+    z = load_golden(name)
+    N, h, r = int(z["N"]), float(z["h"]), float(z["r"])
+    v = z["v"]
+    lap = sh_oracle.lap5(v, N, N, 1.0 / h ** 2)
+    L = sh_oracle.sh13(v, N, N, h, r)
+    assert np.abs(lap - z["lap_v"]).max() <= 1e-13 * np.abs(z["lap_v"]).max()
+    assert np.abs(L - z["L_v"]).max() <= 1e-13 * np.abs(z["L_v"]).max()
+    if N >= 5:
+        assert int(z["L_nnz"]) == 13 * N * N  # 13-point operator (sh_scipy_nk.py:38-39)
+
+
+@pytest.mark.parametrize("name", OPS)
+def test_csr_restatement_matches_reference(name):
+    z = load_golden(name)
+    N, h, r = int(z["N"]), float(z["h"]), float(z["r"])
+    L = sh_oracle.csr_L(N, h, r)
+    assert L.nnz == int(z["L_nnz"])
+    assert np.abs(L @ z["v"] - z["L_v"]).max() <= 1e-13 * np.abs(z["L_v"]).max()
+
+
+def test_residual_matches_reference():
+    z = load_golden("residual_n61")
+    F = sh_oracle.residual(z["u"], z["uo"], 61, 61, float(z["h"]), float(z["r"]), float(z["k"]),
+                           float(z["g"]))
+    assert np.abs(F - z["F"]).max() <= 1e-12 * np.abs(z["F"]).max()
+
+
+def test_jvp_is_derivative_of_residual():
+    z = load_golden("residual_n61")
+    h, r, k, g = float(z["h"]), float(z["r"]), float(z["k"]), float(z["g"])
+    u, uo = z["u"], z["uo"]
+    v = np.random.default_rng(3).standard_normal(u.size)
+    eps = 1e-6
+    fd = (sh_oracle.residual(u + eps * v, uo, 61, 61, h, r, k, g)
+          - sh_oracle.residual(u - eps * v, uo, 61, 61, h, r, k, g)) / (2 * eps)
+    J = sh_oracle.jvp(u, v, 61, 61, h, r, k, g)
+    assert np.abs(J - fd).max() <= 1e-6 * np.abs(J).max()
+
+
+NK = ["nk_n61_default", "nk_n61_tight", "nk_n64_default", "nk_n64_h0625_tight",
+      "nk_n5_d2_tight"]
+
+
+@pytest.mark.parametrize("name", NK)
+@pytest.mark.parametrize("ortho", ["mgs", "icwy"])
+def test_nk_restatement_matches_scipy_steps(name, ortho):
+    z = load_golden(name)
+    N, h, r, k, g = int(z["N"]), float(z["h"]), float(z["r"]), float(z["k"]), float(z["g"])
+    ftol = None if np.isnan(z["f_tol"]) else float(z["f_tol"])
+    traj = z["traj"]
+    for s in range(len(traj) - 1):
+        uo = traj[s]
+        F = lambda u, uo=uo: sh_oracle.residual(u, uo, N, N, h, r, k, g)  # noqa: E731
+        u, st = nk_oracle.newton_krylov(F, uo, f_tol=ftol, return_stats=True, ortho=ortho)
+        ref = traj[s + 1]
+        scale = max(1.0, np.abs(ref).max())
+        tol = 1e-8 if ftol is not None else 1e-5
+        assert np.abs(u - ref).max() <= tol * scale
+        assert abs(st.nit - int(z["nit"][s])) <= 1
+        if ortho == "mgs" and ftol is not None:
+            assert st.nfev == int(z["nfev"][s])
+
+
+def test_nk_restatement_raises_like_scipy():
+    z = load_golden("nk_n61_default")
+    N, h = 61, float(z["h"])
+    uo = z["traj"][0]
+    F = lambda u: sh_oracle.residual(u, uo, N, N, h, 0.01, 0.2, 1.0)  # noqa: E731
+    with pytest.raises(nk_oracle.NoConvergence):
+        nk_oracle.newton_krylov(F, uo, maxiter=1)
