@@ -29,6 +29,7 @@ extern "C" {
 #define NK_NO_CONVERGENCE 1
 #define NK_NONFINITE 2
 #define NK_ZERO_STEP 3
+#define NK_BAD_RHS 4 /* lgmres ValueError 'RHS must contain only finite numbers' (lgmres.py:125) */
 #define NK_EINVAL (-1)
 #define NK_EHIP (-2)
 #define NK_ECOMM (-3)

@@ -71,6 +71,7 @@ const char* nk_status_string(int code) {
     case NK_ZERO_STEP:
       return "Jacobian inversion yielded zero vector. This indicates a bug in the Jacobian "
              "approximation.";
+    case NK_BAD_RHS: return "RHS must contain only finite numbers";
     case NK_EINVAL: return "invalid argument";
     case NK_EHIP: return "HIP runtime error";
     case NK_ECOMM: return "RCCL error";

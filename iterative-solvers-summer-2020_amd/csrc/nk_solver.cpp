@@ -270,6 +270,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   *dmax = 0.0;
   *dvec = nullptr;
   const double b_norm = fx_norm_;
+  if (!std::isfinite(b_norm)) return NK_BAD_RHS;  // lgmres.py:125-126
   if (b_norm == 0.0) return NK_OK;  // x = b = 0  -> zero step
   const double atol = std::max(0.0, tol * b_norm);
   const double r_norm = b_norm;  // r_outer = matvec(0) - b = -b (matvec(0) short-circuits)

@@ -14,6 +14,7 @@ NK_OK = 0
 NK_NO_CONVERGENCE = 1
 NK_NONFINITE = 2
 NK_ZERO_STEP = 3
+NK_BAD_RHS = 4
 NK_EINVAL = -1
 NK_EHIP = -2
 NK_ECOMM = -3

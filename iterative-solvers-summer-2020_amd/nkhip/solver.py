@@ -74,6 +74,8 @@ def raise_for_status(rc: int, x_last=None):
         raise NoConvergence(x_last)
     if rc == _lib.NK_NONFINITE:
         raise ValueError("Function returned non-finite results")
+    if rc == _lib.NK_BAD_RHS:
+        raise ValueError("RHS must contain only finite numbers")
     if rc == _lib.NK_ZERO_STEP:
         raise ValueError("Jacobian inversion yielded zero vector. "
                          "This indicates a bug in the Jacobian approximation.")

@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 passes over the bench (kernel trace + stats, then HBM counters in separate passes).
+# Usage on the GPU box: bash scripts/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}; shift || true
+ARGS=${*:-"--steps 3 --warmup 1 --cpu-baseline off"}
+OUT=$PWD/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # run <name> <timeout> <rocprof args...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$name" -o "$name" --output-format csv -- \
+      python3 bench.py $ARGS > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+run trace 600 --kernel-trace --stats
+run fetch 600 --pmc FETCH_SIZE
+run write 600 --pmc WRITE_SIZE
+find "$OUT" -name "*.csv" | head -20

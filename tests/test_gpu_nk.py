@@ -89,8 +89,13 @@ def test_no_convergence_and_errors():
     F = lambda u: nkhip.sh_residual(u.contiguous(), uo, float(z["h"]), 0.01, 0.2, 1.0, N, N)  # noqa
     with pytest.raises(nkhip.NoConvergence):
         nkhip.newton_krylov(F, uo, maxiter=1)
-    with pytest.raises(ValueError, match="non-finite"):
+    # F = +-inf at x0: scipy's lgmres rejects the right-hand side (lgmres.py:125-126)
+    with pytest.raises(ValueError, match="RHS must contain only finite numbers"):
         nkhip.newton_krylov(lambda u: F(u) / (u - u), uo + 1.0)
+    # finite F(x0) but a non-finite JVP: KrylovJacobian.matvec (_nonlin.py:1511-1512)
+    x_star = uo.clone()
+    with pytest.raises(ValueError, match="non-finite"):
+        nkhip.newton_krylov(lambda u: F(u) + 1e300 * (u - x_star) ** 8 * 1e300, uo)
     with pytest.raises(RuntimeError, match="boom"):
         def bad(u):
             raise RuntimeError("boom")
