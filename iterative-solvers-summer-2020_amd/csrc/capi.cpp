@@ -36,7 +36,7 @@ int reduce_call(int64_t n, int nslots, int nsum, int nv, double* out, hipStream_
   int64_t nblk = 0;
   e = fn(buf, &nblk);
   double* res = buf + size_t(kb) * nslots;
-  if (e == hipSuccess) e = reduce_final_launch(buf, nblk, nsum, nv, res, s);
+  if (e == hipSuccess) e = reduce_final_launch(buf, nblk, nsum, nv, res, nullptr, s);
   if (e == hipSuccess) e = hipMemcpyAsync(out, res, sizeof(double) * nv, hipMemcpyDeviceToHost, s);
   hipFreeAsync(buf, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -28,16 +28,14 @@ struct RcclComm final : nk_comm {
   int rank() const override { return r; }
   int size() const override { return p; }
 
-  int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) override {
+  int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
     if (nsum > 0 && ncclAllReduce(dev, dev, size_t(nsum), ncclDouble, ncclSum, c, s) != ncclSuccess)
       return NK_ECOMM;
     if (nv > nsum &&
         ncclAllReduce(dev + nsum, dev + nsum, size_t(nv - nsum), ncclDouble, ncclMax, c, s) !=
             ncclSuccess)
       return NK_ECOMM;
-    if (hipMemcpyAsync(host, dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)
-      return NK_EHIP;
-    return hipStreamSynchronize(s) == hipSuccess ? NK_OK : NK_EHIP;
+    return NK_OK;
   }
 
   int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
@@ -99,11 +97,13 @@ struct LoopComm final : nk_comm {
   int rank() const override { return r; }
   int size() const override { return sh->p; }
 
-  int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) override {
-    if (hipMemcpyAsync(host, dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess ||
+  int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
+    std::vector<double> host(nv);
+    if (hipMemcpyAsync(host.data(), dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       return NK_EHIP;
-    sh->vals[r].assign(host, host + nv);
+    sh->vals[r] = host;
     sh->wait();
     for (int k = 0; k < nv; ++k) {
       double acc = sh->vals[0][k];
@@ -117,6 +117,10 @@ struct LoopComm final : nk_comm {
       host[k] = acc;
     }
     sh->wait();
+    if (hipMemcpyAsync(dev, host.data(), sizeof(double) * nv, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return NK_EHIP;
     return NK_OK;
   }
 

@@ -15,9 +15,9 @@ struct nk_comm {
   virtual ~nk_comm() = default;
   virtual int rank() const = 0;
   virtual int size() const = 0;
-  // dev[0, nsum) summed and dev[nsum, nv) max-reduced over ranks; the result lands in host[0, nv).
-  // Synchronises `s`.  Returns 0 or a negative NK_E* code.
-  virtual int allreduce(double* dev, double* host, int nsum, int nv, hipStream_t s) = 0;
+  // dev[0, nsum) summed and dev[nsum, nv) max-reduced over ranks, in place in device memory,
+  // ordered on `s` (RCCL: enqueued, no host synchronisation).  Returns 0 or a negative NK_E* code.
+  virtual int allreduce(double* dev, int nsum, int nv, hipStream_t s) = 0;
   // lo <- rows ny_prev-2, ny_prev-1 of the previous rank, hi <- rows 0, 1 of the next rank
   // (periodic ring).  Enqueued on `s` (RCCL) or completed before return (loopback).
   virtual int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,

@@ -41,99 +41,112 @@ __device__ __forceinline__ void st2(double* p, int64_t i, int64_t n, double2 v) 
 
 template <bool VEC>
 __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double* g, VecList P,
-                                                  int np, int64_t n, double* partial) {
+                                                  int np, int64_t n, int cpb, double* partial) {
+  // One block walks `cpb` consecutive 2048-element chunks; per chunk the block keeps its slice of
+  // a (and g) in registers and streams the vectors through it.  Per-vector block sums are
+  // accumulated in LDS, so only one partial per block and value reaches HBM.
+  __shared__ double acc[2 * kMaxVec + 1];
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
-  const int64_t base = bid * kKrylovChunk + 2 * int64_t(threadIdx.x);
-  double2 av[PAIRS], gv[PAIRS];
+  const int nv = 2 * np + 1;
+  for (int t = threadIdx.x; t < nv; t += BS) acc[t] = 0.0;
   double aa = 0.0;
-#pragma unroll
-  for (int k = 0; k < PAIRS; ++k) {
-    av[k] = ld2<VEC>(a, base + k * 2 * BS, n);
-    gv[k] = g ? ld2<VEC>(g, base + k * 2 * BS, n) : make_double2(0.0, 0.0);
-    aa += av[k].x * av[k].x + av[k].y * av[k].y;
-  }
   int buf = 0;
-  for (int i0 = 0; i0 < np; i0 += 4) {
-    double s[8];
+  for (int c = 0; c < cpb; ++c) {
+    const int64_t chunk = bid * cpb + c;
+    if (chunk * kKrylovChunk >= n) break;  // uniform
+    const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
+    double2 av[PAIRS], gv[PAIRS];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] = 0.0;
+    for (int k = 0; k < PAIRS; ++k) {
+      av[k] = ld2<VEC>(a, base + k * 2 * BS, n);
+      gv[k] = g ? ld2<VEC>(g, base + k * 2 * BS, n) : make_double2(0.0, 0.0);
+      aa += av[k].x * av[k].x + av[k].y * av[k].y;
+    }
+    for (int i0 = 0; i0 < np; i0 += 4) {
+      double s[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (i0 + u < np) {
-        const double* p = P.p[i0 + u];
-        double2 pv[PAIRS];
-        if (p == g) {  // the Gram-row vector is already in registers: no second read
+      for (int u = 0; u < 8; ++u) s[u] = 0.0;
 #pragma unroll
-          for (int k = 0; k < PAIRS; ++k) pv[k] = gv[k];
-        } else {
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u < np) {
+          const double* p = P.p[i0 + u];
+          double2 pv[PAIRS];
+          if (p == g) {  // the Gram-row vector is already in registers: no second read
 #pragma unroll
-          for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
-        }
+            for (int k = 0; k < PAIRS; ++k) pv[k] = gv[k];
+          } else {
 #pragma unroll
-        for (int k = 0; k < PAIRS; ++k) {
-          s[u] += av[k].x * pv[k].x + av[k].y * pv[k].y;
-          s[4 + u] += gv[k].x * pv[k].x + gv[k].y * pv[k].y;
+            for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
+          }
+#pragma unroll
+          for (int k = 0; k < PAIRS; ++k) {
+            s[u] += av[k].x * pv[k].x + av[k].y * pv[k].y;
+            s[4 + u] += gv[k].x * pv[k].x + gv[k].y * pv[k].y;
+          }
         }
       }
-    }
-    const double v = block_reduce<8, 8, BS>(s, buf);
-    buf ^= 1;
-    if (threadIdx.x < 8) {
-      const int u = threadIdx.x & 3;
-      if (i0 + u < np) {
-        const int64_t slot = (threadIdx.x < 4) ? (i0 + u) : (np + i0 + u);
-        partial[slot * nblk + bid] = v;
+      const double v = block_reduce<8, 8, BS>(s, buf);
+      buf ^= 1;
+      if (threadIdx.x < 8) {
+        const int u = threadIdx.x & 3;
+        if (i0 + u < np) acc[(threadIdx.x < 4) ? (i0 + u) : (np + i0 + u)] += v;
       }
     }
   }
   double t[1] = {aa};
   const double v = block_reduce<1, 1, BS>(t, buf);
-  if (threadIdx.x == 0) partial[int64_t(2 * np) * nblk + bid] = v;
+  if (threadIdx.x == 0) acc[2 * np] += v;
+  __syncthreads();
+  for (int k = threadIdx.x; k < nv; k += BS) partial[int64_t(k) * nblk + bid] = acc[k];
 }
 
 template <bool VEC>
 __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
-                                                   VecList P, int np, int64_t n,
+                                                   VecList P, int np, int64_t n, int cpb,
                                                    double* partial) {
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
-  const int64_t base = bid * kKrylovChunk + 2 * int64_t(threadIdx.x);
-  double2 acc[PAIRS];
-#pragma unroll
-  for (int k = 0; k < PAIRS; ++k) {
-    if (in) {
-      const double2 x = ld2<VEC>(in, base + k * 2 * BS, n);
-      acc[k] = make_double2(cin * x.x, cin * x.y);
-    } else {
-      acc[k] = make_double2(0.0, 0.0);
-    }
-  }
-#pragma unroll 2
-  for (int i = 0; i < np; ++i) {
-    const double* p = P.p[i];
-    const double c = P.c[i];
-    double2 pv[PAIRS];
-#pragma unroll
-    for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
+  double red[2] = {0.0, 0.0};
+  for (int cc = 0; cc < cpb; ++cc) {
+    const int64_t chunk = bid * cpb + cc;
+    if (chunk * kKrylovChunk >= n) break;  // uniform
+    const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
+    double2 acc[PAIRS];
 #pragma unroll
     for (int k = 0; k < PAIRS; ++k) {
-      acc[k].x += c * pv[k].x;
-      acc[k].y += c * pv[k].y;
+      if (in) {
+        const double2 x = ld2<VEC>(in, base + k * 2 * BS, n);
+        acc[k] = make_double2(cin * x.x, cin * x.y);
+      } else {
+        acc[k] = make_double2(0.0, 0.0);
+      }
     }
-  }
-  double red[2] = {0.0, 0.0};
+#pragma unroll 2
+    for (int i = 0; i < np; ++i) {
+      const double* p = P.p[i];
+      const double c = P.c[i];
+      double2 pv[PAIRS];
 #pragma unroll
-  for (int k = 0; k < PAIRS; ++k) {
-    st2<VEC>(out, base + k * 2 * BS, n, acc[k]);
-    const int64_t i = base + k * 2 * BS;
-    if (i < n) {
-      red[0] += acc[k].x * acc[k].x;
-      red[1] = nmax(red[1], fabs(acc[k].x));
+      for (int k = 0; k < PAIRS; ++k) pv[k] = ld2<VEC>(p, base + k * 2 * BS, n);
+#pragma unroll
+      for (int k = 0; k < PAIRS; ++k) {
+        acc[k].x += c * pv[k].x;
+        acc[k].y += c * pv[k].y;
+      }
     }
-    if (i + 1 < n) {
-      red[0] += acc[k].y * acc[k].y;
-      red[1] = nmax(red[1], fabs(acc[k].y));
+#pragma unroll
+    for (int k = 0; k < PAIRS; ++k) {
+      st2<VEC>(out, base + k * 2 * BS, n, acc[k]);
+      const int64_t i = base + k * 2 * BS;
+      if (i < n) {
+        red[0] += acc[k].x * acc[k].x;
+        red[1] = nmax(red[1], fabs(acc[k].x));
+      }
+      if (i + 1 < n) {
+        red[0] += acc[k].y * acc[k].y;
+        red[1] = nmax(red[1], fabs(acc[k].y));
+      }
     }
   }
   if (partial) {
@@ -143,7 +156,8 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
 }
 
 __global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial, int64_t nblk,
-                                                           int nsum, double* result) {
+                                                           int nsum, double* result,
+                                                           double* result_host) {
   const int k = blockIdx.x;
   const bool is_sum = k < nsum;
   const double* p = partial + int64_t(k) * nblk;
@@ -157,7 +171,10 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial
   } else {
     s = block_reduce<1, 0, 256>(v);
   }
-  if (threadIdx.x == 0) result[k] = s;
+  if (threadIdx.x == 0) {
+    result[k] = s;
+    if (result_host) result_host[k] = s;  // pinned, device-mapped host memory: no D2H blit
+  }
 }
 
 template <bool VEC>
@@ -185,19 +202,29 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
 
+int64_t krylov_grid(int64_t n, int* cpb) {
+  // ~2048 blocks (8 per CU) of 256 threads; each walks ceil(chunks / 2048) chunks.
+  const int64_t chunks = krylov_blocks(n);
+  const int64_t target = 2048;
+  const int64_t c = chunks <= target ? 1 : (chunks + target - 1) / target;
+  *cpb = int(c);
+  return (chunks + c - 1) / c;
+}
+
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
                        double* partial, hipStream_t s, int64_t* nblk) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
-  const int64_t nb = krylov_blocks(n);
+  int cpb = 0;
+  const int64_t nb = krylov_grid(n, &cpb);
   if (nblk) *nblk = nb;
   if (nb == 0) return hipSuccess;
   bool vec = al16(a) && al16(g);
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
   if (vec)
-    hipLaunchKernelGGL(mdot_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n,
+    hipLaunchKernelGGL(mdot_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n, cpb,
                        partial);
   else
-    hipLaunchKernelGGL(mdot_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n,
+    hipLaunchKernelGGL(mdot_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n, cpb,
                        partial);
   return hipGetLastError();
 }
@@ -205,25 +232,26 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
                         int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
-  const int64_t nb = krylov_blocks(n);
+  int cpb = 0;
+  const int64_t nb = krylov_grid(n, &cpb);
   if (nblk) *nblk = nb;
   if (nb == 0) return hipSuccess;
   bool vec = al16(out) && al16(in);
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
   if (vec)
     hipLaunchKernelGGL(combo_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
-                       np, n, partial);
+                       np, n, cpb, partial);
   else
     hipLaunchKernelGGL(combo_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
-                       np, n, partial);
+                       np, n, cpb, partial);
   return hipGetLastError();
 }
 
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,
-                               double* result, hipStream_t s) {
+                               double* result, double* result_host, hipStream_t s) {
   if (nv <= 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_final_kernel, dim3(unsigned(nv)), dim3(256), 0, s, partial, nblk, nsum,
-                     result);
+                     result, result_host);
   return hipGetLastError();
 }
 

@@ -50,6 +50,9 @@ struct StencilArgs {
   SHCoef c{};
   double sc = 1.0;  // FDJVP step
   double* partial = nullptr;  // TRIAL: [3][nblk]
+  // FDJVP/AJVP: if set, the step / scale come from the device value |z_raw|^2 (see jvp_scale)
+  const double* znorm2 = nullptr;
+  double omega = 0.0;
 };
 
 // Launches one stencil pass.  *nblk receives the number of partial-sum slots written (TRIAL).
@@ -71,6 +74,8 @@ constexpr int kKrylovPerThread = 8;
 constexpr int64_t kKrylovChunk = int64_t(kKrylovBlock) * kKrylovPerThread;
 
 inline int64_t krylov_blocks(int64_t n) { return (n + kKrylovChunk - 1) / kKrylovChunk; }
+// Grid of the Krylov kernels: returns the block count, *cpb = 2048-element chunks per block.
+int64_t krylov_grid(int64_t n, int* cpb);
 
 // partial[(i)*nblk + b]: a.p_i for i < np, g.p_i at np+i (g may be null -> zeros), a.a at 2np.
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
@@ -80,8 +85,9 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
                         int64_t n, double* partial, hipStream_t s, int64_t* nblk);
 // result[k] = sum_b partial[k*nblk + b] for k < nsum, NaN-propagating max for nsum <= k < nv.
+// result_host (optional): pinned host memory the kernel also writes (zero-copy readback).
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,
-                               double* result, hipStream_t s);
+                               double* result, double* result_host, hipStream_t s);
 // out = a*x + b*y (y may be null; out may alias x or y).  Element-wise helper of the generic
 // residual path (nk_solve) and of nk_axpy / nk_scal.
 // w = (w - f0) / sc, the finite difference of KrylovJacobian.matvec (_nonlin.py:1509).

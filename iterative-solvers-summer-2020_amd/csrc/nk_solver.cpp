@@ -22,7 +22,7 @@ namespace nk {
 
 namespace {
 constexpr double kEps = DBL_EPSILON;
-constexpr int kReduceSlots = 2 * kMaxVec + 8;
+constexpr int kReduceSlots = Engine::kSlots;
 }  // namespace
 
 nk_opts default_opts() {
@@ -135,28 +135,34 @@ int Engine::copy(double* dst, const double* src, int64_t cnt) {
   });
 }
 
-int Engine::reduce(int64_t nblk, int nsum, int nv, double* out) {
-  if (nv > kReduceSlots) return NK_EINVAL;
-  int rc = launch(K_REDUCE, 8.0 * nblk * nv,
-                  [&] { return reduce_final_launch(partial_, nblk, nsum, nv, dres_, s); });
+int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot) {
+  if (slot < 0 || slot + nv > kReduceSlots) return NK_EINVAL;
+  const bool multi = comm && comm->size() > 1;
+  int rc = launch(K_REDUCE, 8.0 * nblk * nv, [&] {
+    return reduce_final_launch(partial_, nblk, nsum, nv, dres_ + slot,
+                               multi ? nullptr : hres_ + slot, s);
+  });
+  if (rc || !multi) return rc;
+  rc = comm->allreduce(dres_ + slot, nsum, nv, s);
   if (rc) return rc;
-  if (comm && comm->size() > 1) {
-    rc = comm->allreduce(dres_, hres_, nsum, nv, s);
-    if (rc) return rc;
-  } else {
-    if (hipMemcpyAsync(hres_, dres_, sizeof(double) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)
-      return NK_EHIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
-  }
-  harvest();
-  std::memcpy(out, hres_, sizeof(double) * nv);
+  return hipMemcpyAsync(hres_ + slot, dres_ + slot, sizeof(double) * nv, hipMemcpyDeviceToHost,
+                        s) == hipSuccess
+             ? NK_OK
+             : NK_EHIP;
+}
+
+int Engine::reduce(int64_t nblk, int nsum, int nv, double* out) {
+  int rc = reduce_async(nblk, nsum, nv, kSlotSync);
+  if (!rc) rc = sync();
+  if (rc) return rc;
+  std::memcpy(out, hres_ + kSlotSync, sizeof(double) * nv);
   return NK_OK;
 }
 
 // ============================================================================================
 // Newton-Krylov core
 // ============================================================================================
-namespace {
+namespace detail {
 
 void givens(double a, double b, double* c, double* s) {
   if (b == 0.0) {
@@ -236,7 +242,7 @@ void lstsq_upper(const double (*R)[kMaxVec + 1], int n, const double* g, double*
   }
 }
 
-}  // namespace
+}  // namespace detail
 
 NewtonKrylov::NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* external,
                            int64_t external_bytes)
@@ -264,161 +270,7 @@ NewtonKrylov::NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* extern
   orn_.assign(outer_.size(), 0.0);
 }
 
-int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec) {
-  // scipy/sparse/linalg/_isolve/lgmres.py:120-230 with x0 = 0, maxiter = 1, M = identity.
-  *dnorm = 0.0;
-  *dmax = 0.0;
-  *dvec = nullptr;
-  const double b_norm = fx_norm_;
-  if (!std::isfinite(b_norm)) return NK_BAD_RHS;  // lgmres.py:125-126
-  if (b_norm == 0.0) return NK_OK;  // x = b = 0  -> zero step
-  const double atol = std::max(0.0, tol * b_norm);
-  const double r_norm = b_norm;  // r_outer = matvec(0) - b = -b (matvec(0) short-circuits)
-  if (r_norm <= std::max(atol, tol * b_norm)) return NK_OK;
-  const double ptol = std::min(1.0, std::max(atol, tol * b_norm) / r_norm);
-
-  const int n_o = ocount_;
-  const int m = o_.inner_m + n_o;
-  const int64_t n = E_.n;
-  V_[0] = Fx_;  // v0 = b / |b|, kept raw with scale 1/|b|
-  double sig[kMaxVec + 1], rn[kMaxVec + 1];
-  sig[0] = 1.0 / b_norm;
-  rn[0] = b_norm;
-  static thread_local double R[kMaxVec + 1][kMaxVec + 1];
-  static thread_local double gram[kMaxVec + 1][kMaxVec + 1];
-  double cs[kMaxVec + 1], sn[kMaxVec + 1], gv[kMaxVec + 2], hcur[kMaxVec + 2], h[kMaxVec + 1];
-  const double* zp[kMaxVec + 1];
-  double zs[kMaxVec + 1];
-  for (int i = 0; i <= m + 1 && i < kMaxVec + 2; ++i) gv[i] = 0.0;
-  gv[0] = 1.0;
-  double red[kReduceSlots];
-  int j = 0;
-  bool breakdown = false;
-  int rc = NK_OK;
-  for (j = 0; j < m; ++j) {
-    // -- Krylov direction z_j (_gcrotmk.py:107-118 with prepend_outer_v=True)
-    const double* z;
-    double zsig, zrn;
-    if (j < n_o) {
-      const int slot = (ohead_ + j) % int(outer_.size());
-      z = outer_[slot];
-      zsig = osig_[slot];
-      zrn = orn_[slot];
-    } else if (j == n_o) {
-      z = V_[0];
-      zsig = sig[0];
-      zrn = rn[0];
-    } else {
-      z = V_[j];
-      zsig = sig[j];
-      zrn = rn[j];
-    }
-    double* w = V_[j + 1];
-    const double nv = zsig * zrn;  // |z|_2 of the normalised vector (KrylovJacobian.matvec :1506)
-    if (nv == 0.0) {
-      rc = E_.launch(K_COPY, 8.0 * n,
-                     [&] { return hipMemsetAsync(w, 0, sizeof(double) * n, E_.s); });
-    } else {
-      const double sc = omega_ / nv;
-      rc = P_.jvp(X_, G0_, z, zsig, sc, w);
-      st_->njvp += 1;
-    }
-    if (rc) return rc;
-    st_->n_arnoldi += 1;
-    // -- one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i < j), |w|^2
-    VecList P;
-    for (int i = 0; i <= j; ++i) P.p[i] = V_[i];
-    int64_t nblk = 0;
-    const double* g = (j > 0) ? V_[j] : nullptr;
-    rc = E_.launch(K_MDOT, 8.0 * n * (j + 2),
-                   [&] { return mdot_launch(w, g, P, j + 1, n, E_.partial(), E_.s, &nblk); });
-    if (rc) return rc;
-    const int np = j + 1;
-    rc = E_.reduce(nblk, 2 * np + 1, 2 * np + 1, red);
-    if (rc) return rc;
-    const double ww = red[2 * np];
-    if (!std::isfinite(ww)) return NK_NONFINITE;  // _nonlin.py:1511-1512
-    const double w_norm = std::sqrt(ww);
-    for (int i = 0; i < j; ++i) gram[j][i] = sig[j] * sig[i] * red[np + i];
-    // MGS coefficients from the Gram matrix: (I + L) h = V^T w (inverse compact WY form)
-    for (int i = 0; i <= j; ++i) {
-      double acc = sig[i] * red[i];
-      for (int k = 0; k < i; ++k) acc -= gram[i][k] * h[k];
-      h[i] = acc;
-    }
-    VecList U;
-    for (int i = 0; i <= j; ++i) {
-      U.p[i] = V_[i];
-      U.c[i] = -h[i] * sig[i];
-    }
-    rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
-      return combo_launch(w, w, 1.0, U, j + 1, n, E_.partial(), E_.s, &nblk);
-    });
-    if (rc) return rc;
-    rc = E_.reduce(nblk, 1, 2, red);
-    if (rc) return rc;
-    const double hn = std::sqrt(red[0]);
-    for (int i = 0; i <= j; ++i) hcur[i] = h[i];
-    hcur[j + 1] = hn;
-    const double alpha = 1.0 / hn;
-    sig[j + 1] = std::isfinite(alpha) ? alpha : 1.0;
-    rn[j + 1] = hn;
-    if (!(hn > kEps * w_norm)) breakdown = true;
-    zp[j] = z;
-    zs[j] = zsig;
-    // -- Givens update of the Hessenberg QR (qr_insert, _gcrotmk.py:146-158)
-    for (int i = 0; i < j; ++i) {
-      const double t = cs[i] * hcur[i] + sn[i] * hcur[i + 1];
-      hcur[i + 1] = -sn[i] * hcur[i] + cs[i] * hcur[i + 1];
-      hcur[i] = t;
-    }
-    givens(hcur[j], hcur[j + 1], &cs[j], &sn[j]);
-    hcur[j] = cs[j] * hcur[j] + sn[j] * hcur[j + 1];
-    for (int i = 0; i <= j; ++i) R[i][j] = hcur[i];
-    gv[j + 1] = -sn[j] * gv[j];
-    gv[j] = cs[j] * gv[j];
-    const double res = std::fabs(gv[j + 1]);
-    if (res < ptol || breakdown) break;
-  }
-  if (j == m) j = m - 1;
-  if (!std::isfinite(R[j][j])) return NK_OK;  // LinAlgError -> lgmres returns x = 0
-  double y[kMaxVec + 1];
-  lstsq_upper(R, j + 1, gv, y);
-  for (int i = 0; i <= j; ++i) {
-    y[i] *= b_norm;  // y *= inner_res_0
-    if (!std::isfinite(y[i])) return NK_OK;
-  }
-  // -- dx = sum_i y_i z_i into the next outer slot (the oldest one if the ring is full; the
-  //    combination reads each element before writing it, so in-place is safe)
-  const int K = int(outer_.size());
-  const int slot = (o_.outer_k > 0 && ocount_ < o_.outer_k) ? (ohead_ + ocount_) % K : ohead_;
-  VecList Z;
-  for (int i = 0; i <= j; ++i) {
-    Z.p[i] = zp[i];
-    Z.c[i] = y[i] * zs[i];
-  }
-  int64_t nblk = 0;
-  double* d = outer_[slot];
-  rc = E_.launch(K_COMBO, 8.0 * n * (j + 2), [&] {
-    return combo_launch(d, nullptr, 0.0, Z, j + 1, n, E_.partial(), E_.s, &nblk);
-  });
-  if (rc) return rc;
-  rc = E_.reduce(nblk, 1, 2, red);
-  if (rc) return rc;
-  const double nx = std::sqrt(red[0]);
-  if (nx > 0 && o_.outer_k > 0) {
-    osig_[slot] = 1.0 / nx;
-    orn_[slot] = nx;
-    if (ocount_ < o_.outer_k)
-      ++ocount_;
-    else
-      ohead_ = (ohead_ + 1) % K;
-  }
-  *dnorm = nx;
-  *dmax = red[1];
-  *dvec = d;
-  return NK_OK;
-}
+// NewtonKrylov::lgmres lives in lgmres.cpp
 
 int NewtonKrylov::line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax) {
   // _nonlin_line_search(search_type='armijo', smin=1e-2) + scalar_search_armijo(c1=1e-4)

@@ -63,6 +63,15 @@ class Engine {
   // Finish a reduction whose per-block partials are in partial(): values [0,nsum) summed,
   // [nsum,nv) max-reduced, across blocks and ranks; result in out[0,nv).  Synchronises.
   int reduce(int64_t nblk, int nsum, int nv, double* out);
+  // The same without synchronising: the result lands in device slot dres(slot) (ordered on the
+  // stream, all-reduced across ranks) and, after the next sync(), in host slot hres(slot).
+  int reduce_async(int64_t nblk, int nsum, int nv, int slot);
+  const double* dres(int slot) const { return dres_ + slot; }
+  const double* hres(int slot) const { return hres_ + slot; }
+  static constexpr int kSlots = 512;
+  static constexpr int kSlotMdot = 0;     // <= 2*kMaxVec+1 values
+  static constexpr int kSlotCombo = 256;  // 2 values
+  static constexpr int kSlotSync = 384;   // reduce()
   int sync();
   int copy(double* dst, const double* src, int64_t n);
 
@@ -126,6 +135,13 @@ struct Problem {
   // w = J z.  FD: w = (G(x0 + sc*zs*z) - G0)/sc (KrylovJacobian.matvec); analytic: zs*J(x0) z.
   virtual int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
                   double* w) = 0;
+  // As jvp() for z = raw basis vector whose |z|^2 sits in device memory (znorm2): the scale is
+  // computed in-kernel, so no host round trip is needed before the JVP.
+  virtual bool has_dev_scale() const { return false; }
+  virtual int jvp_dev(const double* /*x0*/, const double* /*G0*/, const double* /*z*/,
+                      const double* /*znorm2*/, double /*omega*/, double* /*w*/) {
+    return NK_EINVAL;
+  }
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
 };
@@ -143,6 +159,10 @@ class NewtonKrylov {
 
  private:
   int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
+  // Launch JVP_j (w = V[j+1] = J z_j) and the fused multi-dot of step j; no synchronisation.
+  int issue_step(int j, int n_o, const double* sig, const double* rn, bool dev_scale);
+  const double* zp_[kMaxVec + 1];
+  double zs_[kMaxVec + 1];
   int line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax);
 
   Engine& E_;
@@ -165,5 +185,10 @@ class NewtonKrylov {
 
 // Default options (SciPy newton_krylov defaults).
 nk_opts default_opts();
+
+namespace detail {
+void givens(double a, double b, double* c, double* s);
+void lstsq_upper(const double (*R)[kMaxVec + 1], int n, const double* g, double* y);
+}  // namespace detail
 
 }  // namespace nk

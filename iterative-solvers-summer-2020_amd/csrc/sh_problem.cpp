@@ -117,6 +117,30 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
                    [&] { return stencil_launch(SMode::FDJVP, A, E_.s, nullptr); });
 }
 
+int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
+                       double omega, double* w) {
+  int rc = halo(z, hz_);
+  if (rc) return rc;
+  StencilArgs A;
+  A.ny = ny_;
+  A.nx = nx_;
+  A.c = c_;
+  A.out0 = w;
+  A.znorm2 = znorm2;
+  A.omega = omega;
+  if (jvp_mode_ == NK_JVP_ANALYTIC) {
+    A.a = field(z, hz_);
+    A.p0 = x0;
+    return E_.launch(K_AJVP, stencil_bytes_per_point(SMode::AJVP, false) * ny_ * nx_,
+                     [&] { return stencil_launch(SMode::AJVP, A, E_.s, nullptr); });
+  }
+  A.a = field(x0, hx_);
+  A.b = field(z, hz_);
+  A.p0 = G0;
+  return E_.launch(K_FDJVP, stencil_bytes_per_point(SMode::FDJVP, false) * ny_ * nx_,
+                   [&] { return stencil_launch(SMode::FDJVP, A, E_.s, nullptr); });
+}
+
 // ============================================================================================
 // CallbackProblem
 // ============================================================================================

@@ -21,6 +21,9 @@ class SHProblem final : public Problem {
            double red[3]) override;
   int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
           double* w) override;
+  bool has_dev_scale() const override { return true; }
+  int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
+              double omega, double* w) override;
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
 

@@ -12,6 +12,7 @@
 // The next row is prefetched one iteration ahead.  Requires nx even and 16-B aligned rows.
 // Generic path ("point"): one output per thread with modular indexing (odd nx, e.g. 61x61).
 #include <cmath>
+#include <cstdlib>
 
 #include "nk_device.h"
 #include "nk_kernels.h"
@@ -61,7 +62,8 @@ __device__ __forceinline__ double Gfun(const SHCoef& k, double w, double Lw) {
 }
 
 template <SMode M>
-__device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const Nb& nb, double pv) {
+__device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const Nb& nb, double pv,
+                                      double alpha, double sc) {
   Res r{0.0, 0.0, 0.0};
   const SHCoef& k = A.c;
   if constexpr (M == SMode::LAP5) {
@@ -83,10 +85,10 @@ __device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const 
     r.o1 = G;
     r.o2 = na.c;
   } else if constexpr (M == SMode::FDJVP) {
-    r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) / A.sc;
+    r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) / sc;
   } else {  // AJVP
     const double z = na.c, u = pv;
-    r.o0 = A.alpha * (z / k.k - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
+    r.o0 = alpha * (z / k.k - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
   }
   return r;
 }
@@ -99,6 +101,28 @@ template <SMode M>
 constexpr bool kHasP0 = (M == SMode::TRIAL || M == SMode::FDJVP || M == SMode::AJVP);
 template <SMode M>
 constexpr int kRad = (M == SMode::LAP5) ? 1 : 2;
+
+// JVP scale: either from the host (A.alpha, A.sc) or, when A.znorm2 is set, from the device
+// norm |z_raw|^2 left by the previous fused update (KrylovJacobian.matvec with v = z_raw/|z_raw|:
+// sc = omega/|v|, step = sc/|z_raw|), so the host need not synchronise before the JVP.
+template <SMode M>
+__device__ __forceinline__ void jvp_scale(const StencilArgs& A, double* alpha, double* sc) {
+  *alpha = A.alpha;
+  *sc = A.sc;
+  if constexpr (M == SMode::FDJVP || M == SMode::AJVP) {
+    if (A.znorm2) {
+      const double hn = sqrt(*A.znorm2);
+      double sig = 1.0 / hn;
+      if (!isfinite(sig)) sig = 1.0;
+      if constexpr (M == SMode::FDJVP) {
+        *sc = A.omega / (sig * hn);
+        *alpha = *sc * sig;
+      } else {
+        *alpha = sig;
+      }
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------------
 // march kernel
@@ -114,6 +138,8 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   const int64_t cc = active ? c0 : 0;
   const int64_t cm = (cc >= 2) ? cc - 2 : cc - 2 + nx;
   const int64_t cp = (cc + 2 < nx) ? cc + 2 : cc + 2 - nx;
+  double alpha, sc;
+  jvp_scale<M>(A, &alpha, &sc);
 
   auto ld = [&](const Field& f, int64_t r, double (&v)[6]) {
     const double* p = rowp(f, r, ny, nx);
@@ -128,7 +154,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
       double t[6];
       ld(A.b, r, t);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) va[q] = va[q] + A.alpha * t[q];
+      for (int q = 0; q < 6; ++q) va[q] = va[q] + alpha * t[q];
     } else if constexpr (kTwo<M>) {
       ld(A.b, r, vb);
     }
@@ -170,7 +196,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
         a.dg = 0.0;
         a.a2 = 0.0;
       }
-      res[q] = finish<M>(A, a, b, q == 0 ? pv.x : pv.y);
+      res[q] = finish<M>(A, a, b, q == 0 ? pv.x : pv.y, alpha, sc);
     }
     if (active) {
       *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
@@ -217,6 +243,8 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
   const int64_t nx = A.nx, ny = A.ny;
   const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
   const bool active = idx < nx * ny;
+  double alpha, sc;
+  jvp_scale<M>(A, &alpha, &sc);
   double red[3] = {0.0, 0.0, 0.0};
   if (active) {
     const int64_t i = idx / nx, j = idx % nx;
@@ -230,7 +258,7 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
     };
     auto wv = [&](int64_t di, int64_t dj) {
       double v = val(A.a, di, dj);
-      if constexpr (kComb<M>) v = v + A.alpha * val(A.b, di, dj);
+      if constexpr (kComb<M>) v = v + alpha * val(A.b, di, dj);
       return v;
     };
     Nb a, b{0.0, 0.0, 0.0, 0.0};
@@ -251,7 +279,7 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
     }
     double pv = 0.0;
     if constexpr (kHasP0<M>) pv = A.p0[idx];
-    const Res res = finish<M>(A, a, b, pv);
+    const Res res = finish<M>(A, a, b, pv, alpha, sc);
     A.out0[idx] = res.o0;
     if constexpr (M == SMode::TRIAL) {
       A.out1[idx] = res.o1;
@@ -269,6 +297,11 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
 bool field_ok(const Field& f) {
   return f.base == nullptr ||
          (aligned16(f.base) && (f.lo == nullptr || (aligned16(f.lo) && aligned16(f.hi))));
@@ -280,11 +313,15 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
                     aligned16(A.p0) && aligned16(A.out0) && aligned16(A.out1) && aligned16(A.out2);
   if (fast) {
     // Row band per block: aim for >= ~2048 blocks (8 per CU) with bands of 4..32 rows.
+    // (NKHIP_RY_MIN / NKHIP_RY_MAX / NKHIP_BLOCKS override the choice for tuning runs.)
+    static const int ry_min = env_int("NKHIP_RY_MIN", 4);
+    static const int ry_max = env_int("NKHIP_RY_MAX", 32);
+    static const int blocks = env_int("NKHIP_BLOCKS", 2048);
     constexpr int BX = 128;
     const int64_t gx = (A.nx / 2 + BX - 1) / BX;
-    int64_t ry = (A.ny * gx) / 2048;
-    int RY = 4;
-    while (RY < 32 && RY * 2 <= ry) RY *= 2;
+    int64_t ry = (A.ny * gx) / blocks;
+    int RY = ry_min;
+    while (RY < ry_max && RY * 2 <= ry) RY *= 2;
     const int64_t gy = (A.ny + RY - 1) / RY;
     if (gy > 65535) return hipErrorInvalidValue;
     if (nblk) *nblk = gx * gy;
