@@ -123,7 +123,7 @@ def main():
         model.step(a, out=b)
         a, b = b, a
     model.reset_profile()
-    tot = {"nit": 0, "nfev": 0, "njvp": 0}
+    tot = {"nit": 0, "nfev": 0, "njvp": 0, "n_arnoldi": 0}
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -177,6 +177,7 @@ def main():
             "newton_its_per_s": round(tot["nit"] / elapsed, 3),
             "jvps_per_s": round(tot["njvp"] / elapsed, 2),
             "per_step": {k_: v / args.steps for k_, v in tot.items()},
+            "ms_per_arnoldi_step": round(1e3 * elapsed / max(tot["njvp"], 1), 4),
             "roofline": roof(dom),
             "jvp_roofline": roof(jvp_name) if jvp_name in ker else None,
             "kernel_time_frac_of_wall": round(kernel_ms * 1e-3 / elapsed, 4),

@@ -10,6 +10,7 @@
 // LDS round, then a deterministic second-stage kernel (fixed summation order, so a run is
 // bit-reproducible).
 #include <cmath>
+#include <cstdlib>
 
 #include "nk_device.h"
 #include "nk_kernels.h"
@@ -202,10 +203,14 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
 
-int64_t krylov_grid(int64_t n, int* cpb) {
-  // ~2048 blocks (8 per CU) of 256 threads; each walks ceil(chunks / 2048) chunks.
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+int64_t krylov_grid(int64_t n, int* cpb, int64_t target) {
+  // at most `target` blocks of 256 threads; each walks ceil(chunks / target) chunks.
   const int64_t chunks = krylov_blocks(n);
-  const int64_t target = 2048;
   const int64_t c = chunks <= target ? 1 : (chunks + target - 1) / target;
   *cpb = int(c);
   return (chunks + c - 1) / c;
@@ -214,8 +219,9 @@ int64_t krylov_grid(int64_t n, int* cpb) {
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
                        double* partial, hipStream_t s, int64_t* nblk) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
+  static const int target = env_int("NKHIP_MDOT_BLOCKS", 1024);
   int cpb = 0;
-  const int64_t nb = krylov_grid(n, &cpb);
+  const int64_t nb = krylov_grid(n, &cpb, target);
   if (nblk) *nblk = nb;
   if (nb == 0) return hipSuccess;
   bool vec = al16(a) && al16(g);
@@ -232,8 +238,9 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
                         int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
+  static const int target = env_int("NKHIP_COMBO_BLOCKS", 1 << 30);
   int cpb = 0;
-  const int64_t nb = krylov_grid(n, &cpb);
+  const int64_t nb = krylov_grid(n, &cpb, target);
   if (nblk) *nblk = nb;
   if (nb == 0) return hipSuccess;
   bool vec = al16(out) && al16(in);

@@ -75,7 +75,7 @@ constexpr int64_t kKrylovChunk = int64_t(kKrylovBlock) * kKrylovPerThread;
 
 inline int64_t krylov_blocks(int64_t n) { return (n + kKrylovChunk - 1) / kKrylovChunk; }
 // Grid of the Krylov kernels: returns the block count, *cpb = 2048-element chunks per block.
-int64_t krylov_grid(int64_t n, int* cpb);
+int64_t krylov_grid(int64_t n, int* cpb, int64_t target_blocks);
 
 // partial[(i)*nblk + b]: a.p_i for i < np, g.p_i at np+i (g may be null -> zeros), a.a at 2np.
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
