@@ -81,6 +81,15 @@ def cpu_baseline(n, h, k, r, g, fevals_per_step):
     }
 
 
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "latest_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -146,14 +155,25 @@ def main():
         ker = {k_: v for k_, v in prof.items() if v["launches"] > 0 and v["ms"] > 0}
         dom = max(ker, key=lambda k_: ker[k_]["ms"])
 
+        traffic_db = load_traffic()
+
         def roof(name):
             v = ker[name]
             gbs = v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9
+            alg = v["alg_bytes"] / v["launches"]
+            t = traffic_db.get("classes", {}).get(name)
+            traffic = None
+            if t and "traffic_over_alg" in t:
+                # PMC HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) per launch, measured
+                # on the same kernel class by scripts/profile.sh; scaled to this run's launches by
+                # the traffic/algorithmic ratio of the profiled run.
+                traffic = round(t["traffic_over_alg"] * alg)
             return {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                    "traffic": None, "launches": v["launches"],
+                    "traffic": traffic, "launches": v["launches"],
                     "avg_us": round(1e3 * v["ms"] / v["launches"], 2),
-                    "alg_bytes_per_launch": v["alg_bytes"] / v["launches"]}
+                    "alg_bytes_per_launch": alg,
+                    "traffic_source": traffic_db.get("source") if traffic else None}
 
         jvp_name = "sh_fdjvp" if args.jvp == "fd" else "sh_ajvp"
         kernel_ms = sum(v["ms"] for v in ker.values())
