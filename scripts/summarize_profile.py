@@ -52,7 +52,7 @@ def main():
                 bench = json.loads(line)
     out = [f"# rocprofv3 summary `{tag}`", "",
            "Command: `scripts/profile.sh` = `rocprofv3 --kernel-trace --stats` over "
-           "`python3 bench.py " + (" ".join(sys.argv[2:]) or "--steps 3 --warmup 1 --cpu-baseline off")
+           "`python3 bench.py " + (" ".join(sys.argv[2:]) or "--steps 3 --warmup 0 --cpu-baseline off")
            + "`, then two separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes.", "",
            "| kernel | calls | avg us (rocprof) | % time | HBM read MB/launch (2x FETCH_SIZE) "
            "| HBM write MB/launch |", "|---|---|---|---|---|---|"]
