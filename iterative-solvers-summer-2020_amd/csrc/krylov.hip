@@ -46,13 +46,14 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   // One block walks `cpb` consecutive 2048-element chunks; per chunk the block keeps its slice of
   // a (and g) in registers and streams the vectors through it.  Per-vector block sums are
   // accumulated in LDS, so only one partial per block and value reaches HBM.
-  __shared__ double acc[2 * kMaxVec + 1];
+  __shared__ double accw[BS / 64][2 * kMaxVec + 1];
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
   const int nv = 2 * np + 1;
-  for (int t = threadIdx.x; t < nv; t += BS) acc[t] = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int t = lane; t < nv; t += 64) accw[wid][t] = 0.0;  // each wave zeroes its own slice
   double aa = 0.0;
-  int buf = 0;
   for (int c = 0; c < cpb; ++c) {
     const int64_t chunk = bid * cpb + c;
     if (chunk * kKrylovChunk >= n) break;  // uniform
@@ -87,19 +88,30 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
           }
         }
       }
-      const double v = block_reduce<8, 8, BS>(s, buf);
-      buf ^= 1;
-      if (threadIdx.x < 8) {
-        const int u = threadIdx.x & 3;
-        if (i0 + u < np) acc[(threadIdx.x < 4) ? (i0 + u) : (np + i0 + u)] += v;
+      // wave-level sums only (no block barrier inside the streaming loop); each wave keeps its
+      // own LDS accumulators, combined once at the end
+      wave_sum<8>(s);
+      if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (i0 + u < np) {
+            accw[wid][i0 + u] += s[u];
+            accw[wid][np + i0 + u] += s[4 + u];
+          }
+        }
       }
     }
   }
   double t[1] = {aa};
-  const double v = block_reduce<1, 1, BS>(t, buf);
-  if (threadIdx.x == 0) acc[2 * np] += v;
+  wave_sum<1>(t);
+  if (lane == 0) accw[wid][2 * np] += t[0];
   __syncthreads();
-  for (int k = threadIdx.x; k < nv; k += BS) partial[int64_t(k) * nblk + bid] = acc[k];
+  for (int k = threadIdx.x; k < nv; k += BS) {
+    double v = accw[0][k];
+#pragma unroll
+    for (int w = 1; w < BS / 64; ++w) v += accw[w][k];
+    partial[int64_t(k) * nblk + bid] = v;
+  }
 }
 
 template <bool VEC>

@@ -13,6 +13,16 @@ __device__ __forceinline__ double nmax(double a, double b) {
   return (b != b || b > a) ? b : a;
 }
 
+// Sum NV values over the 64 lanes of a wave (xor butterfly); every lane ends with the sums.
+template <int NV>
+__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], o, 64);
+  }
+}
+
 // Reduce NV values over a 1-D block of BS threads: the first NSUM values are summed, the rest
 // max-reduced (NaN-propagating).  Wave64 xor-shuffle tree, then one LDS round across waves.
 // Returns value `threadIdx.x` to the threads with threadIdx.x < NV (others get 0).

@@ -171,21 +171,36 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
 
   double wa[NR][6], wb[NB][6];
   double na_[6], nb_[6];
+  // Odd bands march upwards: a band boundary is then reached by both adjacent bands at the same
+  // time (both at their start or both at their end), so the halo rows one band re-reads are still
+  // in L2.  The window sums below pair the rows symmetrically about the centre, so the result is
+  // bitwise the same in either direction (fp addition is commutative).
   const int64_t r0 = int64_t(blockIdx.y) * RY;
   const int64_t r1 = (r0 + RY < ny) ? r0 + RY : ny;
+  const bool up = (blockIdx.y & 1) != 0;
+  const int64_t dir = up ? -1 : 1;
+  const int64_t rs = up ? r1 - 1 : r0;
 #pragma unroll
-  for (int m = 0; m < NR; ++m) ldw(r0 - R + m, wa[m], wb[kTwo<M> ? m : 0]);
+  for (int m = 0; m < NR; ++m) ldw(rs + dir * (m - R), wa[m], wb[kTwo<M> ? m : 0]);
 
   double red[3] = {0.0, 0.0, 0.0};
-  for (int64_t r = r0; r < r1; ++r) {
+  // the point-wise input is prefetched one row ahead as well, so that the compute of row r waits
+  // only for loads issued during the previous iteration (in-order vmcnt)
+  double2 pv_next = make_double2(0.0, 0.0);
+  if constexpr (kHasP0<M>) pv_next = *reinterpret_cast<const double2*>(A.p0 + rs * nx + cc);
+  for (int64_t it = 0; it < r1 - r0; ++it) {
+    const int64_t r = rs + dir * it;
     const int64_t o = r * nx + cc;
-    // point-wise input first (in-order vmcnt: the compute below then waits only for it and for
-    // the rows prefetched one iteration earlier, not for the prefetch issued next)
-    double2 pv = make_double2(0.0, 0.0);
-    if constexpr (kHasP0<M>) pv = *reinterpret_cast<const double2*>(A.p0 + o);
+    const double2 pv = pv_next;
+    if constexpr (kHasP0<M>) {
+      int64_t rp = r + dir;
+      rp = (rp >= ny) ? ny - 1 : ((rp < 0) ? 0 : rp);
+      pv_next = *reinterpret_cast<const double2*>(A.p0 + rp * nx + cc);
+    }
     // prefetch the next entering row (unconditionally: past the band end it re-reads a valid
     // halo row, which keeps the load count per iteration fixed for the waitcnt schedule)
-    const int64_t rn = (r + R + 1 <= ny + 1) ? r + R + 1 : ny + 1;
+    int64_t rn = r + dir * (R + 1);
+    rn = (rn > ny + 1) ? ny + 1 : ((rn < -2) ? -2 : rn);
     ldw(rn, na_, nb_);
     Res res[2];
 #pragma unroll
@@ -193,18 +208,18 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
       Nb a, b{0.0, 0.0, 0.0, 0.0};
       if constexpr (R == 2) {
         a.c = wa[2][2 + q];
-        a.a1 = wa[2][1 + q] + wa[2][3 + q] + wa[1][2 + q] + wa[3][2 + q];
-        a.dg = wa[1][1 + q] + wa[1][3 + q] + wa[3][1 + q] + wa[3][3 + q];
-        a.a2 = wa[2][q] + wa[2][4 + q] + wa[0][2 + q] + wa[4][2 + q];
+        a.a1 = (wa[2][1 + q] + wa[2][3 + q]) + (wa[1][2 + q] + wa[3][2 + q]);
+        a.dg = (wa[1][1 + q] + wa[1][3 + q]) + (wa[3][1 + q] + wa[3][3 + q]);
+        a.a2 = (wa[2][q] + wa[2][4 + q]) + (wa[0][2 + q] + wa[4][2 + q]);
         if constexpr (kTwo<M>) {
           b.c = wb[2][2 + q];
-          b.a1 = wb[2][1 + q] + wb[2][3 + q] + wb[1][2 + q] + wb[3][2 + q];
-          b.dg = wb[1][1 + q] + wb[1][3 + q] + wb[3][1 + q] + wb[3][3 + q];
-          b.a2 = wb[2][q] + wb[2][4 + q] + wb[0][2 + q] + wb[4][2 + q];
+          b.a1 = (wb[2][1 + q] + wb[2][3 + q]) + (wb[1][2 + q] + wb[3][2 + q]);
+          b.dg = (wb[1][1 + q] + wb[1][3 + q]) + (wb[3][1 + q] + wb[3][3 + q]);
+          b.a2 = (wb[2][q] + wb[2][4 + q]) + (wb[0][2 + q] + wb[4][2 + q]);
         }
       } else {
         a.c = wa[1][2 + q];
-        a.a1 = wa[1][1 + q] + wa[1][3 + q] + wa[0][2 + q] + wa[2][2 + q];
+        a.a1 = (wa[1][1 + q] + wa[1][3 + q]) + (wa[0][2 + q] + wa[2][2 + q]);
         a.dg = 0.0;
         a.a2 = 0.0;
       }
@@ -275,19 +290,19 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
     };
     Nb a, b{0.0, 0.0, 0.0, 0.0};
     a.c = wv(0, 0);
-    a.a1 = wv(0, -1) + wv(0, 1) + wv(-1, 0) + wv(1, 0);
+    a.a1 = (wv(0, -1) + wv(0, 1)) + (wv(-1, 0) + wv(1, 0));
     if constexpr (R == 2) {
-      a.dg = wv(-1, -1) + wv(-1, 1) + wv(1, -1) + wv(1, 1);
-      a.a2 = wv(0, -2) + wv(0, 2) + wv(-2, 0) + wv(2, 0);
+      a.dg = (wv(-1, -1) + wv(-1, 1)) + (wv(1, -1) + wv(1, 1));
+      a.a2 = (wv(0, -2) + wv(0, 2)) + (wv(-2, 0) + wv(2, 0));
     } else {
       a.dg = 0.0;
       a.a2 = 0.0;
     }
     if constexpr (kTwo<M>) {
       b.c = val(A.b, 0, 0);
-      b.a1 = val(A.b, 0, -1) + val(A.b, 0, 1) + val(A.b, -1, 0) + val(A.b, 1, 0);
-      b.dg = val(A.b, -1, -1) + val(A.b, -1, 1) + val(A.b, 1, -1) + val(A.b, 1, 1);
-      b.a2 = val(A.b, 0, -2) + val(A.b, 0, 2) + val(A.b, -2, 0) + val(A.b, 2, 0);
+      b.a1 = (val(A.b, 0, -1) + val(A.b, 0, 1)) + (val(A.b, -1, 0) + val(A.b, 1, 0));
+      b.dg = (val(A.b, -1, -1) + val(A.b, -1, 1)) + (val(A.b, 1, -1) + val(A.b, 1, 1));
+      b.a2 = (val(A.b, 0, -2) + val(A.b, 0, 2)) + (val(A.b, -2, 0) + val(A.b, 2, 0));
     }
     double pv = 0.0;
     if constexpr (kHasP0<M>) pv = A.p0[idx];
