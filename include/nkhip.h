@@ -150,6 +150,42 @@ int nk_solve(nk_residual_fn F, void* ctx, const double* x0_dev, double* x_dev, i
              const nk_opts* opts, nk_stats* stats, void* stream, void* workspace,
              int64_t workspace_bytes);
 
+/* ---------------- thin-film droplet on a moving mesh (python_work/droplet.py, config 3) -------- */
+/* Parameters = the module globals of droplet.py:22-53 (defaults from nk_drop_params_default). */
+typedef struct nk_drop_params {
+  int32_t nx, ny;                 /* 91, 61 (:29) */
+  double endl, endr, endb, endt;  /* -3, 6, -3, 3 (:32-33) */
+  double epsilon;                 /* precursor film 1e-2 (:24) */
+  int32_t n_exp, m_exp;           /* 6, 3 (:48-49) */
+  double Bo, alpha2;              /* 0.01, 0 (:47, :50) */
+  double alpha, gamma, C;         /* PMA: 0.01, 0.1, 0.15 (:40-42) */
+  int32_t smoothing_iters;        /* 4 (:31) */
+  int32_t pad_;
+} nk_drop_params;
+typedef struct nk_drop nk_drop;
+
+int nk_drop_params_default(nk_drop_params* p);
+int nk_drop_create(nk_drop** out, const nk_drop_params* p, const nk_opts* opts, void* stream);
+int nk_drop_destroy(nk_drop* d);
+/* state: U.new (= U.val) and the mesh potential Q.val, device arrays of nx*ny */
+int nk_drop_set_state(nk_drop* d, const double* U_dev, const double* Q_dev);
+int nk_drop_get_state(nk_drop* d, double* U_dev, double* Q_dev);
+/* one iteration of evolve_with_PDE (droplet.py:369-411): dt_n = dt*scale; U.val = U.new; the
+ * mesh / old-time fields; U.new = newton_krylov(residual(u, F, dt_n), U.val) with the nk_opts
+ * given at creation (the reference: maxiter=20, f_tol=1e-7, :383); loop_pma(dtmesh, pmaloops);
+ * scale += exp(-10 |U.new - U.val|).  *dt_used = dt_n, *scale = the updated scale. */
+int nk_drop_step(nk_drop* d, double dt, double dtmesh, int32_t pmaloops, nk_stats* stats,
+                 double* dt_used, double* scale);
+int nk_drop_set_scale(nk_drop* d, double scale);
+/* pieces of the step (tests / tooling): */
+int nk_drop_prepare(nk_drop* d);  /* droplet.py:371-381 for the current state (U.val = U.new) */
+/* which: 0 d2ksi 1 d2eta 2 dksideta 3 J 4 A11 5 A22 6 A12 7 Q_dksi 8 Q_deta 9 F 10 U.xx 11 U.yy
+ *        12 U.val 13 U.new 14 Q.val */
+int nk_drop_field(nk_drop* d, int32_t which, double* out_dev);
+int nk_drop_residual(nk_drop* d, const double* u_dev, double dt, double* R_dev); /* :435-450 */
+int nk_drop_solve(nk_drop* d, double dt, double* U_dev, nk_stats* stats);         /* :383 */
+int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops);                       /* :589-599 */
+
 #ifdef __cplusplus
 }
 #endif

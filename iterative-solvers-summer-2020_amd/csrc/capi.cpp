@@ -11,6 +11,7 @@
 #include "comm.h"
 #include "nk_kernels.h"
 #include "nk_solver.h"
+#include "droplet_problem.h"
 #include "sh_problem.h"
 
 using namespace nk;
@@ -323,6 +324,102 @@ int nk_solve(nk_residual_fn F, void* ctx, const double* x0, double* x, int64_t n
   hipStreamSynchronize(S(stream));
   if (own) hipFree(ws);
   return rc;
+}
+
+// ------------------------------------------------------------------------------ droplet
+int nk_drop_params_default(nk_drop_params* p) {
+  if (!p) return NK_EINVAL;
+  *p = nk_drop_params{};
+  p->nx = 91;
+  p->ny = 61;
+  p->endl = -3;
+  p->endr = 6;
+  p->endb = -3;
+  p->endt = 3;
+  p->epsilon = 1e-2;
+  p->n_exp = 6;
+  p->m_exp = 3;
+  p->Bo = 0.01;
+  p->alpha2 = 0.0;
+  p->alpha = 0.01;
+  p->gamma = 0.1;
+  p->C = 0.15;
+  p->smoothing_iters = 4;
+  return NK_OK;
+}
+
+int nk_drop_create(nk_drop** out, const nk_drop_params* p, const nk_opts* opts, void* stream) {
+  if (!out || !p || p->nx < 7 || p->ny < 7) return NK_EINVAL;
+  DropParams P{};
+  P.nx = p->nx;
+  P.ny = p->ny;
+  P.endl = p->endl;
+  P.endr = p->endr;
+  P.endb = p->endb;
+  P.endt = p->endt;
+  P.dksi = (p->endr - p->endl) / (p->nx - 1);  // droplet.py:36
+  P.deta = (p->endt - p->endb) / (p->ny - 1);  // :37
+  P.epsilon = p->epsilon;
+  P.n_exp = p->n_exp;
+  P.m_exp = p->m_exp;
+  P.Bo = p->Bo;
+  P.alpha2 = p->alpha2;
+  P.epsilon2 = 1.0 / (p->endt - p->endb);  // :51
+  P.alpha = p->alpha;
+  P.gamma = p->gamma;
+  P.C = p->C;
+  P.smoothing_iters = p->smoothing_iters;
+  const nk_opts o = opts ? *opts : default_opts();
+  std::unique_ptr<DropletStepper> d(new (std::nothrow) DropletStepper(P, o, S(stream)));
+  if (!d) return NK_ENOMEM;
+  if (d->status()) return d->status();
+  *out = reinterpret_cast<nk_drop*>(d.release());
+  return NK_OK;
+}
+
+static DropletStepper* DS(nk_drop* d) { return reinterpret_cast<DropletStepper*>(d); }
+
+int nk_drop_destroy(nk_drop* d) {
+  delete DS(d);
+  return NK_OK;
+}
+int nk_drop_set_state(nk_drop* d, const double* U, const double* Q) {
+  return (d && U && Q) ? DS(d)->set_state(U, Q) : NK_EINVAL;
+}
+int nk_drop_get_state(nk_drop* d, double* U, double* Q) {
+  return d ? DS(d)->get_state(U, Q) : NK_EINVAL;
+}
+int nk_drop_step(nk_drop* d, double dt, double dtmesh, int32_t pmaloops, nk_stats* stats,
+                 double* dt_used, double* scale) {
+  if (!d || pmaloops < 0) return NK_EINVAL;
+  const int rc = DS(d)->step(dt, dtmesh, pmaloops, stats, dt_used);
+  if (scale) *scale = DS(d)->scale;
+  return rc;
+}
+int nk_drop_set_scale(nk_drop* d, double scale) {
+  if (!d) return NK_EINVAL;
+  DS(d)->scale = scale;
+  return NK_OK;
+}
+int nk_drop_prepare(nk_drop* d) {
+  if (!d) return NK_EINVAL;
+  int rc = DS(d)->E.copy(DS(d)->P.uval, DS(d)->P.unew, DS(d)->E.n);
+  if (!rc) rc = DS(d)->prepare();
+  return rc ? rc : DS(d)->E.sync();
+}
+int nk_drop_field(nk_drop* d, int32_t which, double* out) {
+  return (d && out) ? DS(d)->field(which, out) : NK_EINVAL;
+}
+int nk_drop_residual(nk_drop* d, const double* u, double dt, double* R) {
+  return (d && u && R) ? DS(d)->residual(u, dt, R) : NK_EINVAL;
+}
+int nk_drop_solve(nk_drop* d, double dt, double* U, nk_stats* stats) {
+  return (d && U) ? DS(d)->solve(dt, U, stats) : NK_EINVAL;
+}
+int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops) {
+  if (!d || loops < 1) return NK_EINVAL;
+  const int rc = DS(d)->pma(dtmesh, loops);
+  return rc ? rc : DS(d)->E.sync();
 }
 
 }  // extern "C"

@@ -1,0 +1,69 @@
+// Thin-film droplet (python_work/droplet.py) on a mapped 2-D mesh: device kernels.
+//
+// The grid is small (91 x 61 = 5551 points in the reference, config 3), so every operator chain
+// runs as ONE single-workgroup kernel whose stages are separated by workgroup barriers, with the
+// intermediate fields in L2-resident scratch: one launch per residual evaluation instead of the
+// reference's 10 sparse mat-vecs and ~60 NumPy passes (droplet.py:435-450).
+//
+// Layout: u[i*nx + j], i = eta row (ny), j = xi column (nx); Left/Right = columns 0/nx-1,
+// Bottom/Top = rows 0/ny-1 (make_Ibdy, droplet.py:762-776).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace nk {
+
+struct DropParams {
+  int nx, ny;
+  double dksi, deta;
+  double endl, endr, endb, endt;  // domain limits (droplet.py:32-33)
+  double epsilon;                 // precursor film (:24)
+  int n_exp, m_exp;               // disjoining-pressure exponents (:48-49)
+  double Bo, alpha2, epsilon2;    // Bond number, inclination, Ho/Lo (:47,50-51)
+  double alpha, gamma, C;         // PMA: adaption speed, smoothing, Mackenzie constant (:40-42)
+  int smoothing_iters;            // (:31)
+};
+
+// Per-time-step fields of the mesh potential Q (compute_Q_spatial_ders :696-711, J :376) and
+// the Laplace metric coefficients A11, A22, A12 (:612-614).
+struct DropMesh {
+  double *d2ksi, *d2eta, *dksideta, *J, *A11, *A22, *A12;
+  double *dksi, *deta;  // Q_xi, Q_eta = the physical node coordinates x, y
+};
+
+// Scratch fields of the staged kernels (8 arrays of nx*ny doubles).
+struct DropScratch {
+  double *w, *ud, *ue, *t1, *t2, *p, *A, *B;
+};
+
+// Q -> DropMesh (one single-workgroup launch).
+hipError_t drop_mesh_launch(const DropParams& P, const double* q, DropMesh M, hipStream_t s);
+
+// Old-time quantities of evolve_with_PDE (:371-381): U.xx, U.yy (Laplacian with the
+// compute_u_spatial_ders boundary rules, incl. the U_dksi[Bottom] quirk :722) and the CN term
+// F = pde_rhs(U.val, U.xx, U.yy).
+hipError_t drop_rhs_launch(const DropParams& P, const double* uval, DropMesh M, DropScratch S,
+                           double* uxx, double* uyy, double* F, hipStream_t s);
+
+// residual(w, F, dt) (:435-450) at w = x + alpha*y (y may be null).
+//   mode 0: out = R(w); also xt <- w (if non-null) and partial[0..2] = sum R^2, max|R|, max|w|
+//   mode 1: out = (R(w) - f0) / sc  (the finite-difference JVP of KrylovJacobian.matvec)
+hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, const double* x,
+                             const double* y, double alpha, const double* uval, const double* F,
+                             double dt, int mode, const double* f0, double sc, double* out,
+                             double* xt, double* partial, hipStream_t s);
+
+// The PMA mesh loop loop_pma(dtm, loops) (:589-599) in one persistent single-workgroup launch.
+// The first iteration uses the caller's u_xx, u_yy (and the mesh fields in M); q is updated in
+// place.  Cx (nx*nx), Cy (ny*ny): orthonormal DCT-II matrices; den: 1 - gamma*Leig (ny*nx).
+hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, double* q,
+                           const double* uval, const double* uxx0, const double* uyy0,
+                           const double* Cx, const double* Cy, const double* den, double dtm,
+                           int loops, hipStream_t s);
+void drop_pma_tables(const DropParams& P, std::vector<double>* cx, std::vector<double>* cy,
+                     std::vector<double>* den);
+
+}  // namespace nk

@@ -44,6 +44,14 @@ class nk_kprof(C.Structure):
                 ("alg_bytes", C.c_double)]
 
 
+class nk_drop_params(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("endl", C.c_double), ("endr", C.c_double),
+                ("endb", C.c_double), ("endt", C.c_double), ("epsilon", C.c_double),
+                ("n_exp", C.c_int32), ("m_exp", C.c_int32), ("Bo", C.c_double),
+                ("alpha2", C.c_double), ("alpha", C.c_double), ("gamma", C.c_double),
+                ("C", C.c_double), ("smoothing_iters", C.c_int32), ("pad_", C.c_int32)]
+
+
 RESIDUAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
 
 _P = C.c_void_p
@@ -83,6 +91,20 @@ SIGNATURES = [
     ("nk_solve_workspace_bytes", C.c_int64, [_I64, C.POINTER(nk_opts)]),
     ("nk_solve", C.c_int, [RESIDUAL_FN, _P, _P, _P, _I64, C.POINTER(nk_opts),
                            C.POINTER(nk_stats), _P, _P, _I64]),
+    ("nk_drop_params_default", C.c_int, [C.POINTER(nk_drop_params)]),
+    ("nk_drop_create", C.c_int, [C.POINTER(_P), C.POINTER(nk_drop_params), C.POINTER(nk_opts),
+                                 _P]),
+    ("nk_drop_destroy", C.c_int, [_P]),
+    ("nk_drop_set_state", C.c_int, [_P, _P, _P]),
+    ("nk_drop_get_state", C.c_int, [_P, _P, _P]),
+    ("nk_drop_step", C.c_int, [_P, _D, _D, _I32, C.POINTER(nk_stats), C.POINTER(_D),
+                               C.POINTER(_D)]),
+    ("nk_drop_set_scale", C.c_int, [_P, _D]),
+    ("nk_drop_prepare", C.c_int, [_P]),
+    ("nk_drop_field", C.c_int, [_P, _I32, _P]),
+    ("nk_drop_residual", C.c_int, [_P, _P, _D, _P]),
+    ("nk_drop_solve", C.c_int, [_P, _D, _P, C.POINTER(nk_stats)]),
+    ("nk_drop_pma", C.c_int, [_P, _D, _I32]),
 ]
 
 
