@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--n", type=int, default=4096, help="grid points per side")
     ap.add_argument("--jvp", choices=["fd", "analytic"], default="fd")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--extra", choices=["on", "off"], default="on",
+                    help="also measure configs 2 (1024^2 Lap SpMV) and 3 (91x61 droplet)")
     return ap.parse_args()
 
 
@@ -79,6 +81,73 @@ def cpu_baseline(n, h, k, r, g, fevals_per_step):
                    f"csr_matvec and NumPy element-wise are single-threaded; OpenBLAS BLAS-1 uses "
                    f"{blas_threads} threads; os.cpu_count()={os.cpu_count()}"),
     }
+
+
+def config2_lap5(n=1024, reps=200):
+    """Config 2: 1024^2 fp64 periodic 5-point Laplacian SpMV (sh_scipy_nk.py:32-35), 16 B/pt,
+    timed with HIP events on torch's stream; the reference's CSR `Lap @ v` timed beside it."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    from oracle import sh_oracle
+    h = 0.625
+    v_np = np.random.default_rng(7).standard_normal(n * n)
+    v = torch.as_tensor(v_np.reshape(n, n), device="cuda")
+    y = torch.empty_like(v)
+    for _ in range(5):
+        nkhip.lap5_apply(v, 1 / h ** 2, out=y)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        nkhip.lap5_apply(v, 1 / h ** 2, out=y)
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / reps
+    err = float(np.abs(y.cpu().numpy().reshape(-1) - sh_oracle.lap5(v_np, n, n, 1 / h ** 2)).max())
+    L = sh_oracle.csr_lap(n, h)
+    best = 1e9
+    for _ in range(20):
+        t0 = time.perf_counter()
+        L @ v_np
+        best = min(best, time.perf_counter() - t0)
+    return {"workload": f"lap5_{n}x{n}_fp64", "avg_us_per_launch_incl_gap": round(us, 2),
+            "alg_GBps": round(16 * n * n / (us * 1e-6) / 1e9, 1), "max_abs_err_vs_oracle": err,
+            "cpu_scipy_csr_ms": round(best * 1e3, 3),
+            "note": "back-to-back launches; the per-kernel duration is in profiles/*_summary.md"}
+
+
+def config3_droplet(steps=5, cpu_steps=2):
+    """Config 3: 91x61 droplet time-march (droplet.py evolve_with_PDE, 400 PMA loops per step)
+    from the reference's coal init state; the restated reference path (scipy) timed beside it."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    from oracle import droplet_oracle
+    with np.load(os.path.join(ROOT, "tests", "golden", "droplet_init.npz")) as z:
+        U0, Q0 = z["U0"], z["Q0"]
+    d = nkhip.Droplet()
+    d.set_state(U0, Q0)
+    d.step()  # warm-up (compiles nothing, but pages in the kernels)
+    d.set_state(U0, Q0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nits = 0
+    for _ in range(steps):
+        d.step(1e-4, 3e-9, 400)
+        nits += d.last_stats["nit"]
+    torch.cuda.synchronize()
+    gpu = time.perf_counter() - t0
+    d.close()
+    t0 = time.perf_counter()
+    droplet_oracle.evolve(U0, Q0, cpu_steps)
+    cpu = time.perf_counter() - t0
+    return {"workload": "droplet_91x61_coal_evolve_with_PDE", "steps": steps,
+            "gpu_steps_per_s": round(steps / gpu, 2), "newton_its_per_step": nits / steps,
+            "cpu_reference_path_steps_per_s": round(cpu_steps / cpu, 3), "cpu_steps": cpu_steps,
+            "pma_loops_per_step": 400}
 
 
 def load_traffic():
@@ -210,6 +279,8 @@ def main():
         if world == 1 and args.cpu_baseline == "auto":
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
             out["cpu_baseline"] = cpu_baseline(n, h, k, r, g, fe)
+        if world == 1 and args.extra == "on":
+            out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet()}
         print(json.dumps(out), flush=True)
     model.close()
     if comm is not None:

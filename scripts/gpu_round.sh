@@ -16,7 +16,7 @@ for s in "$@"; do
     tests)  step pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
     alltests) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench)  step bench 900 python bench.py --steps 5 --warmup 1 --cpu-baseline off ;;
+    bench)  step bench 900 python bench.py --steps 5 --warmup 1 --cpu-baseline off --extra off ;;
     benchfull) step bench_full 900 python bench.py ;;
   esac
 done

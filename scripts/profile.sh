@@ -3,7 +3,7 @@
 # Usage on the GPU box: bash scripts/profile.sh <tag> [bench args...]
 set -u
 TAG=${1:-r01}; shift || true
-ARGS=${*:-"--steps 3 --warmup 0 --cpu-baseline off"}
+ARGS=${*:-"--steps 3 --warmup 0 --cpu-baseline off --extra off"}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
