@@ -56,14 +56,22 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s);
 
+// Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
+// Cy (ny*ny), their transposes, and den = 1 - gamma*Leig (ny*nx).  Packed in one allocation of
+// drop_pma_table_size() doubles, each matrix followed by kPmaPad zeros (tile over-reads).
+struct PmaTables {
+  const double *cx, *cxt, *cy, *cyt, *den;
+};
+constexpr int kPmaPad = 8;
+size_t drop_pma_table_size(const DropParams& P);
+std::vector<double> drop_pma_tables(const DropParams& P);
+PmaTables drop_pma_view(const DropParams& P, const double* packed);
+
 // The PMA mesh loop loop_pma(dtm, loops) (:589-599) in one persistent single-workgroup launch.
 // The first iteration uses the caller's u_xx, u_yy (and the mesh fields in M); q is updated in
-// place.  Cx (nx*nx), Cy (ny*ny): orthonormal DCT-II matrices; den: 1 - gamma*Leig (ny*nx).
+// place.
 hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, double* q,
                            const double* uval, const double* uxx0, const double* uyy0,
-                           const double* Cx, const double* Cy, const double* den, double dtm,
-                           int loops, hipStream_t s);
-void drop_pma_tables(const DropParams& P, std::vector<double>* cx, std::vector<double>* cy,
-                     std::vector<double>* den);
+                           const PmaTables& T, double dtm, int loops, hipStream_t s);
 
 }  // namespace nk

@@ -6,6 +6,9 @@
 // matrices of make_M (droplet.py:778-833) are applied matrix-free with their exact coefficients
 // (integer weights divided by 12*h or 12*h^2, as the reference builds them).
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "droplet.h"
@@ -15,120 +18,120 @@ namespace nk {
 namespace {
 
 constexpr int DB = 1024;
+constexpr size_t kPmaLdsMax = 156 * 1024;  // dynamic LDS cap (160 KB per CU minus static use)
 
-// One 1-D derivative operator (a kron factor of make_M): interior weights at offsets -2..2 and
-// explicit rows for the two outermost points at each end.
-struct Op1 {
-  double in[5];
-  double r0[6], r1[6], rm2[6], rm1[6];  // rows 0, 1, n-2, n-1
-  int n0, n1, nm2, nm1;                 // entries in those rows (rows n-2/n-1 end at column n-1)
-};
+int env_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : 0;
+}
 
+// The four 1-D derivative operators (kron factors of make_M, droplet.py:778-833): 0 = D1 along
+// xi, 1 = D1 along eta (dksiCentre / detaCentre, :795-806), 2 / 3 = D2 along xi / eta (d2ksi /
+// d2eta, :782-793).  Entries are the reference's weights divided by s = 12h (D1) or 12h^2 (D2).
+// The 5-point interior weights travel as a small kernel argument (SGPR-resident); the two
+// boundary rows at each end live in a per-launch LDS table built by coef_rows_init, so a kernel
+// never holds the ~100 boundary weights in scalar registers.
 struct Coefs {
-  Op1 d1x, d1y, d2x, d2y;
+  double in[4][5];
+  double s[4];
 };
+constexpr int kCoefRows = 4 * 4 * 6;
+__shared__ double g_rows[kCoefRows];  // [op][row 0, 1, n-2, n-1][6], filled per launch
 
-Op1 make_d1(double h) {
-  // dksiCentre / detaCentre factor (:795-806)
-  Op1 o{};
-  const double s = 12 * h;
-  const double in[5] = {1, -8, 0, 8, -1};
-  const double r0[5] = {-25, 48, -36, 16, -3}, r1[5] = {-3, -10, 18, -6, 1};
-  const double rm2[5] = {-1, 6, -18, 10, 3}, rm1[5] = {3, -16, 36, -48, 25};
-  for (int k = 0; k < 5; ++k) {
-    o.in[k] = in[k] / s;
-    o.r0[k] = r0[k] / s;
-    o.r1[k] = r1[k] / s;
-    o.rm2[k] = rm2[k] / s;
-    o.rm1[k] = rm1[k] / s;
+// Boundary-row weights before division (row lengths 5, 5, 5, 5 for D1 and 5, 6, 6, 5 for D2;
+// rows n-2 / n-1 end at column n-1).
+__constant__ double kRowW[2][4][6] = {
+    {{-25, 48, -36, 16, -3, 0}, {-3, -10, 18, -6, 1, 0}, {-1, 6, -18, 10, 3, 0},
+     {3, -16, 36, -48, 25, 0}},
+    {{-415.0 / 6, 96, -36, 32.0 / 3, -1.5, 0}, {10, -15, -4, 14, -6, 1}, {1, -6, 14, -4, -15, 10},
+     {-1.5, 32.0 / 3, -36, 96, -415.0 / 6, 0}}};
+
+__device__ __forceinline__ void coef_rows_init(const Coefs& C) {
+  for (int t = threadIdx.x; t < kCoefRows; t += DB) {
+    const int op = t / 24, row = (t / 6) % 4, k = t % 6;
+    const double sc = op == 0 ? C.s[0] : op == 1 ? C.s[1] : op == 2 ? C.s[2] : C.s[3];
+    g_rows[t] = kRowW[op >= 2][row][k] / sc;  // selects: no dynamic index into the argument
   }
-  o.n0 = o.n1 = o.nm2 = o.nm1 = 5;
-  return o;
+  __syncthreads();
 }
 
-Op1 make_d2(double h2) {
-  // d2ksi / d2eta factor (:782-793)
-  Op1 o{};
-  const double s = 12 * h2;
-  const double in[5] = {-1, 16, -30, 16, -1};
-  const double r0[5] = {-415.0 / 6, 96, -36, 32.0 / 3, -1.5};
-  const double r1[6] = {10, -15, -4, 14, -6, 1};
-  const double rm2[6] = {1, -6, 14, -4, -15, 10};
-  const double rm1[5] = {-1.5, 32.0 / 3, -36, 96, -415.0 / 6};
-  for (int k = 0; k < 5; ++k) {
-    o.in[k] = in[k] / s;
-    o.r0[k] = r0[k] / s;
-    o.rm1[k] = rm1[k] / s;
-  }
-  for (int k = 0; k < 6; ++k) {
-    o.r1[k] = r1[k] / s;
-    o.rm2[k] = rm2[k] / s;
-  }
-  o.n0 = 5;
-  o.n1 = 6;
-  o.nm2 = 6;
-  o.nm1 = 5;
-  return o;
-}
-
-// Apply a 1-D operator at position `pos` of an axis of length n; element k of the axis is
-// v[k*stride].
-__device__ __forceinline__ double op1(const Op1& o, const double* v, int pos, int n, int stride) {
-  double acc = 0.0;
-  if (pos >= 2 && pos <= n - 3) {
-    acc = o.in[0] * v[(pos - 2) * stride] + o.in[1] * v[(pos - 1) * stride];
-    if (o.in[2] != 0.0) acc += o.in[2] * v[pos * stride];
-    acc += o.in[3] * v[(pos + 1) * stride] + o.in[4] * v[(pos + 2) * stride];
+// Apply operator OP at position `pos` of an axis of length n; element k of the axis is
+// v[k*stride].  Summation runs over the row's columns in increasing order (CSR row order).
+template <int OP, bool kIn = false>
+__device__ __forceinline__ double op1(const Coefs& C, const double* v, int pos, int n, int stride) {
+  constexpr bool kD2 = OP >= 2;
+  const double* in = C.in[OP];
+  double acc;
+  if (kIn || (pos >= 2 && pos <= n - 3)) {
+    acc = in[0] * v[(pos - 2) * stride] + in[1] * v[(pos - 1) * stride];
+    if (kD2) acc += in[2] * v[pos * stride];  // the D1 centre weight is zero
+    acc += in[3] * v[(pos + 1) * stride] + in[4] * v[(pos + 2) * stride];
     return acc;
   }
+  const double* r = g_rows + OP * 24;
+  constexpr int L1 = kD2 ? 6 : 5;
+  acc = 0.0;
   if (pos == 0) {
-    for (int k = 0; k < o.n0; ++k) acc += o.r0[k] * v[k * stride];
+#pragma nounroll
+    for (int k = 0; k < 5; ++k) acc += r[k] * v[k * stride];
   } else if (pos == 1) {
-    for (int k = 0; k < o.n1; ++k) acc += o.r1[k] * v[k * stride];
+#pragma nounroll
+    for (int k = 0; k < L1; ++k) acc += r[6 + k] * v[k * stride];
   } else if (pos == n - 2) {
-    for (int k = 0; k < o.nm2; ++k) acc += o.rm2[k] * v[(n - o.nm2 + k) * stride];
+#pragma nounroll
+    for (int k = 0; k < L1; ++k) acc += r[12 + k] * v[(n - L1 + k) * stride];
   } else {
-    for (int k = 0; k < o.nm1; ++k) acc += o.rm1[k] * v[(n - o.nm1 + k) * stride];
+#pragma nounroll
+    for (int k = 0; k < 5; ++k) acc += r[18 + k] * v[(n - 5 + k) * stride];
   }
   return acc;
 }
 
-__device__ __forceinline__ double dx1(const Coefs& C, const double* v, int i, int j, int nx) {
-  return op1(C.d1x, v + i * nx, j, nx, 1);
+// Derivatives of a field stored row-major with row stride `ld` (nx for global fields, the padded
+// LDS stride for staged ones).
+template <bool kIn = false>
+__device__ __forceinline__ double dx1(const Coefs& C, const double* v, int i, int j, int nx,
+                                      int ld) {
+  return op1<0, kIn>(C, v + i * ld, j, nx, 1);
 }
-__device__ __forceinline__ double dy1(const Coefs& C, const double* v, int i, int j, int nx,
-                                      int ny) {
-  return op1(C.d1y, v + j, i, ny, nx);
+template <bool kIn = false>
+__device__ __forceinline__ double dy1(const Coefs& C, const double* v, int i, int j, int ny,
+                                      int ld) {
+  return op1<1, kIn>(C, v + j, i, ny, ld);
 }
 
 // M.dksideta = kron(D1y, D1x) (:806): sum over the row operator of the column-derivatives.
+template <bool kIn = false>
 __device__ __forceinline__ double dxy(const Coefs& C, const double* v, int i, int j, int nx,
-                                      int ny) {
-  const Op1& o = C.d1y;
+                                      int ny, int ld) {
   double acc = 0.0;
-  if (i >= 2 && i <= ny - 3) {
-    for (int k = -2; k <= 2; ++k)
-      if (o.in[k + 2] != 0.0) acc += o.in[k + 2] * dx1(C, v, i + k, j, nx);
+  if (kIn || (i >= 2 && i <= ny - 3)) {
+    const double* in = C.in[1];
+    acc += in[0] * dx1<kIn>(C, v, i - 2, j, nx, ld);  // row order, zero centre weight skipped
+    acc += in[1] * dx1<kIn>(C, v, i - 1, j, nx, ld);
+    acc += in[3] * dx1<kIn>(C, v, i + 1, j, nx, ld);
+    acc += in[4] * dx1<kIn>(C, v, i + 2, j, nx, ld);
     return acc;
   }
-  const double* w;
-  int cnt, start;
-  if (i == 0) { w = o.r0; cnt = o.n0; start = 0; }
-  else if (i == 1) { w = o.r1; cnt = o.n1; start = 0; }
-  else if (i == ny - 2) { w = o.rm2; cnt = o.nm2; start = ny - o.nm2; }
-  else { w = o.rm1; cnt = o.nm1; start = ny - o.nm1; }
-  for (int k = 0; k < cnt; ++k) acc += w[k] * dx1(C, v, start + k, j, nx);
+  const double* r = g_rows + 24;
+  int start = 0;
+  if (i == 1) r += 6;
+  if (i == ny - 2) { r += 12; start = ny - 5; }
+  if (i == ny - 1) { r += 18; start = ny - 5; }
+#pragma nounroll
+  for (int k = 0; k < 5; ++k) acc += r[k] * dx1<kIn>(C, v, start + k, j, nx, ld);
   return acc;
 }
 
 // The explicit part of Laplace_operator along one axis (:616-668): v_xx (axis = x, A = A11) or
 // v_yy (axis = y, A = A22) at position `pos` of a line of length n, element k at v[k*stride].
+template <bool kIn = false>
 __device__ __forceinline__ double lap_axis(const double* v, const double* A, int pos, int n,
                                            int s, double h2) {
   auto V = [&](int k) { return v[k * s]; };
   auto a = [&](int k) { return A[k * s]; };
   const int m = pos;
-  if (m >= 3 && m <= n - 4) {  // interior (:617-631)
+  if (kIn || (m >= 3 && m <= n - 4)) {  // interior (:617-631)
     return (4 * (a(m - 1) * (V(m - 3) - 8 * V(m - 2) + 8 * V(m) - V(m + 1)))
             - ((-a(m - 2) + 9 * a(m - 1) + 9 * a(m) - a(m + 1)) *
                (V(m - 2) - 27 * V(m - 1) + 27 * V(m) - V(m + 1)))
@@ -174,18 +177,46 @@ __device__ __forceinline__ double pressure(const DropParams& P, double h, double
   return -(hxx + hyy) + PI(P, h) + P.Bo * cos(P.alpha2) * h;  // (:469-473)
 }
 
-#define FOR_POINTS(NN)                                                     \
-  for (int p_ = threadIdx.x; p_ < (NN); p_ += DB)                          \
-    if (const int i_ = p_ / nx, j_ = p_ - i_ * nx; true)
+// Visit every grid point once: the deep interior (3 <= i <= ny-4, 3 <= j <= nx-4, where every
+// operator takes its 5-point interior form) first, branch-free (kIn = true), then the 3-wide
+// boundary ring with the general per-position code.  Only the one wave straddling the split
+// diverges; a row-major walk would put boundary columns in nearly every wave.
+template <class F>
+__device__ __forceinline__ void for_points(int nx, int ny, F f) {
+  const int ix = nx - 6, iy = ny - 6, nI = ix * iy, NN = nx * ny;
+  for (int t = threadIdx.x; t < NN; t += DB) {
+    if (t < nI) {
+      const int i = 3 + t / ix, j = 3 + t % ix;
+      f(i * nx + j, i, j, std::true_type{});
+    } else {
+      int u = t - nI, i, j;
+      if (u < 6 * nx) {  // rows 0-2 and ny-3..ny-1
+        const int r = u / nx;
+        i = r < 3 ? r : ny - 6 + r;
+        j = u - r * nx;
+      } else {  // columns 0-2 and nx-3..nx-1 of rows 3..ny-4
+        u -= 6 * nx;
+        const int c = u / iy;
+        j = c < 3 ? c : nx - 6 + c;
+        i = 3 + (u - c * iy);
+      }
+      f(i * nx + j, i, j, std::false_type{});
+    }
+  }
+}
+#define FOR_POINTS(NN) \
+  for_points(nx, ny, [&](const int p_, const int i_, const int j_, auto kin_)
 
 // ---------------------------------------------------------------------------- kernels
-__device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q, const DropMesh& M) {
+__device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q, int ldq,
+                           const DropMesh& M, double* a11 = nullptr, double* a22 = nullptr) {
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   // compute_Q_spatial_ders (:696-711), J (:376) and the Laplace metric (:612-614): point-wise
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_, i = i_, j = j_;
     const bool left = j == 0, right = j == nx - 1, bottom = i == 0, top = i == ny - 1;
-    double qd = dx1(C, q, i, j, nx), qe = dy1(C, q, i, j, nx, ny);
+    double qd = dx1<kIn>(C, q, i, j, nx, ldq), qe = dy1<kIn>(C, q, i, j, ny, ldq);
     if (left) qd = P.endl;
     if (right) qd = P.endr;
     if (bottom) qe = P.endb;
@@ -193,12 +224,12 @@ __device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q,
     double t = 0.0;
     if (left) t = 25 / (6 * P.dksi) * fabs(P.endl);
     if (right) t = 25 / (6 * P.dksi) * fabs(P.endr);
-    const double q2x = op1(C.d2x, q + i * nx, j, nx, 1) + t;
+    const double q2x = op1<2, kIn>(C, q + i * ldq, j, nx, 1) + t;
     t = 0.0;
     if (top) t = 25 / (6 * P.deta) * fabs(P.endt);
     if (bottom) t = 25 / (6 * P.deta) * fabs(P.endb);
-    const double q2y = op1(C.d2y, q + j, i, ny, nx) + t;
-    const double qxy = (left || right || top || bottom) ? 0.0 : dxy(C, q, i, j, nx, ny);
+    const double q2y = op1<3, kIn>(C, q + j, i, ny, ldq) + t;
+    const double qxy = (left || right || top || bottom) ? 0.0 : dxy<kIn>(C, q, i, j, nx, ny, ldq);
     const double J = q2x * q2y - qxy * qxy;
     M.dksi[p] = qd;
     M.deta[p] = qe;
@@ -206,31 +237,39 @@ __device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q,
     M.d2eta[p] = q2y;
     M.dksideta[p] = qxy;
     M.J[p] = J;
-    M.A11[p] = (qxy * qxy + q2y * q2y) / J;
-    M.A22[p] = (qxy * qxy + q2x * q2x) / J;
+    const double A11 = (qxy * qxy + q2y * q2y) / J, A22 = (qxy * qxy + q2x * q2x) / J;
+    M.A11[p] = A11;
+    M.A22[p] = A22;
+    if (a11) {
+      a11[i * ldq + j] = A11;
+      a22[i * ldq + j] = A22;
+    }
     M.A12[p] = -(qxy * (q2x + q2y)) / J;
-  }
+  });
 }
 
-__global__ void __launch_bounds__(DB) drop_mesh_kernel(DropParams P, Coefs C, const double* q,
+__global__ void __launch_bounds__(DB) drop_mesh_kernel(DropParams P, Coefs Ck, const double* q,
                                                        DropMesh M) {
-  mesh_stage(P, C, q, M);
+  const Coefs& C = Ck;
+  coef_rows_init(C);
+  mesh_stage(P, C, q, P.nx, M);
 }
 
 // compute_u_spatial_ders (:713-727) first half: u_xi, u_eta with its boundary rules, incl. the
 // U_dksi[Bottom] quirk (:722), as the cross-term inputs t1 = A12 u_eta, t2 = A12 u_xi.
 __device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                            const DropScratch& S, const double* u) {
+                            const DropScratch& S, const double* u, int ldu) {
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_, i = i_, j = j_;
-    double ud = dx1(C, u, i, j, nx), ue = dy1(C, u, i, j, nx, ny);
+    double ud = dx1<kIn>(C, u, i, j, nx, ldu), ue = dy1<kIn>(C, u, i, j, ny, ldu);
     if (j == 0 || j == nx - 1) ud = 0.0;
     if (i == ny - 1) ue = 0.0;
     if (i == 0) ud = 0.0;
     S.t1[p] = M.A12[p] * ue;
     S.t2[p] = M.A12[p] * ud;
-  }
+  });
 }
 
 // The shared tail of the residual / pde_rhs chains, given u (point values) in `u`:
@@ -238,32 +277,42 @@ __device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh&
 //   stage P: p derivatives with dp/dn = 0 -> p_x, p_y -> A, B
 //   stage F: F2 = J^-1 [d2eta A_xi - dksideta A_eta - dksideta B_xi + d2ksi B_eta]
 // The caller has filled S.ud / S.ue (u derivatives with its own boundary rules), S.t1, S.t2.
+// `u`, `a11`, `a22` share the row stride `ld`.  With `mon` set (the PMA loop) the stage writes the
+// raw monitor |u_xx + u_yy|^2 (:737) there instead of the pressure.
 __device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                                   const DropScratch& S, const double* u, double* uxx,
-                                   double* uyy) {
+                                   const DropScratch& S, const double* u, const double* a11,
+                                   const double* a22, int ld, double* uxx, double* uyy,
+                                   double* mon = nullptr) {
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_, i = i_, j = j_;
-    const double vxx = lap_axis(u + i * nx, M.A11 + i * nx, j, nx, 1, P.dksi * P.dksi);
-    const double vyy = lap_axis(u + j, M.A22 + j, i, ny, nx, P.deta * P.deta);
-    double tx = dx1(C, S.t1, i, j, nx);
+    const double vxx = lap_axis<kIn>(u + i * ld, a11 + i * ld, j, nx, 1, P.dksi * P.dksi);
+    const double vyy = lap_axis<kIn>(u + j, a22 + j, i, ny, ld, P.deta * P.deta);
+    double tx = dx1<kIn>(C, S.t1, i, j, nx, nx);
     if (j == 0 || j == nx - 1) tx = 0.0;
-    double ty = dy1(C, S.t2, i, j, nx, ny);
+    double ty = dy1<kIn>(C, S.t2, i, j, ny, nx);
     if (i == 0 || i == ny - 1) ty = 0.0;
     const double hxx = (vxx + tx) / M.J[p];
     const double hyy = (vyy + ty) / M.J[p];
     if (uxx) uxx[p] = hxx;
     if (uyy) uyy[p] = hyy;
-    S.p[p] = pressure(P, u[p], hxx, hyy);
-  }
+    if (mon) {
+      const double s = fabs(hxx + hyy);
+      mon[p] = s * s;
+    } else {
+      S.p[p] = pressure(P, u[i * ld + j], hxx, hyy);
+    }
+  });
 }
 
 __device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
                               const DropScratch& S, const double* u) {
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_, i = i_, j = j_;
-    double pd = dx1(C, S.p, i, j, nx), pe = dy1(C, S.p, i, j, nx, ny);
+    double pd = dx1<kIn>(C, S.p, i, j, nx, nx), pe = dy1<kIn>(C, S.p, i, j, ny, nx);
     if (j == 0 || j == nx - 1) pd = 0.0;
     if (i == 0 || i == ny - 1) pe = 0.0;
     const double pdx = (M.d2eta[p] * pd - M.dksideta[p] * pe) / M.J[p];
@@ -271,60 +320,69 @@ __device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMes
     const double h3 = pow(u[p], 3.0);
     S.A[p] = (pdx - P.Bo * sin(P.alpha2) / P.epsilon2) * h3 / 3;
     S.B[p] = pdy * h3 / 3;
-  }
+  });
 }
 
+template <bool kIn>
 __device__ __forceinline__ double flux_div_point(const Coefs& C, const DropMesh& M,
                                                  const DropScratch& S, int p, int i, int j,
                                                  int nx, int ny) {
-  return (M.d2eta[p] * dx1(C, S.A, i, j, nx) - M.dksideta[p] * dy1(C, S.A, i, j, nx, ny)
-          - M.dksideta[p] * dx1(C, S.B, i, j, nx) + M.d2ksi[p] * dy1(C, S.B, i, j, nx, ny)) /
+  return (M.d2eta[p] * dx1<kIn>(C, S.A, i, j, nx, nx) - M.dksideta[p] * dy1<kIn>(C, S.A, i, j, ny, nx)
+          - M.dksideta[p] * dx1<kIn>(C, S.B, i, j, nx, nx) + M.d2ksi[p] * dy1<kIn>(C, S.B, i, j, ny, nx)) /
          M.J[p];
 }
 
-__global__ void __launch_bounds__(DB) drop_rhs_kernel(DropParams P, Coefs C, DropMesh M,
+__global__ void __launch_bounds__(DB) drop_rhs_kernel(DropParams P, Coefs Ck, DropMesh M,
                                                       DropScratch S, const double* u,
                                                       double* uxx, double* uyy, double* F) {
+  const Coefs& C = Ck;
+  coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  uders_stage(P, C, M, S, u);
+  uders_stage(P, C, M, S, u, nx);
   __syncthreads();
-  lap_pressure_stage(P, C, M, S, u, uxx, uyy);  // P.val = pressure(U.val, U.xx, U.yy) (:378)
+  lap_pressure_stage(P, C, M, S, u, M.A11, M.A22, nx, uxx, uyy);  // P.val = pressure(U.val, U.xx, U.yy) (:378)
   __syncthreads();
   flux_AB_stage(P, C, M, S, u);  // compute_P_spatial_ders (:683-694), pde_rhs A, B (:456-457)
   __syncthreads();
-  FOR_POINTS(NN) { F[p_] = flux_div_point(C, M, S, p_, i_, j_, nx, ny); }
+  FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; F[p_] = flux_div_point<kIn>(C, M, S, p_, i_, j_, nx, ny); });
 }
 
-__global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs C, DropMesh M,
+__global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, DropMesh M,
                                                         DropScratch S, const double* x,
                                                         const double* y, double alpha,
                                                         const double* uval, const double* F,
                                                         double dt, int mode, const double* f0,
                                                         double sc, double* out, double* xt,
                                                         double* partial) {
+  const Coefs& C = Ck;
+  coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     double w = x[p_];
     if (y) w = w + alpha * y[p_];
     S.w[p_] = w;
-  }
+  });
   __syncthreads();
   // residual() feeds the raw derivatives to Laplace_operator (:437, no boundary rules)
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_, i = i_, j = j_;
-    const double ud = dx1(C, S.w, i, j, nx), ue = dy1(C, S.w, i, j, nx, ny);
+    const double ud = dx1<kIn>(C, S.w, i, j, nx, nx), ue = dy1<kIn>(C, S.w, i, j, ny, nx);
     S.t1[p] = M.A12[p] * ue;
     S.t2[p] = M.A12[p] * ud;
-  }
+  });
   __syncthreads();
-  lap_pressure_stage(P, C, M, S, S.w, nullptr, nullptr);
+  lap_pressure_stage(P, C, M, S, S.w, M.A11, M.A22, nx, nullptr, nullptr);
   __syncthreads();
   flux_AB_stage(P, C, M, S, S.w);
   __syncthreads();
   double red[3] = {0.0, 0.0, 0.0};
   FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
     const int p = p_;
-    const double F2 = flux_div_point(C, M, S, p, i_, j_, nx, ny);
+    const double F2 = flux_div_point<kIn>(C, M, S, p, i_, j_, nx, ny);
     const double w = S.w[p];
     const double R = (w - uval[p]) - dt * (F2 + F[p]) / 2;  // (:450)
     if (mode == 0) {
@@ -336,7 +394,7 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs C, D
     } else {
       out[p] = (R - f0[p]) / sc;
     }
-  }
+  });
   if (mode == 0) {
     const double v = block_reduce<3, 1, DB>(red);
     if (threadIdx.x < 3) partial[threadIdx.x] = v;
@@ -348,11 +406,64 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs C, D
 // persistent single-workgroup kernel running all `loops` iterations on the GPU.  The orthonormal
 // DCT-II / -III (scipy.fft dct / idct, norm="ortho") are dense products with precomputed DCT
 // matrices (91x91 and 61x61 at the reference size).
-__global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs C, DropMesh M, DropScratch S,
-                                                      double* q, const double* uval,
+
+// One pass of the 9-point monitor filter (:740-756), T -> Mo, both with row stride ld.
+__device__ void smooth_pass(const DropParams& P, const double* T, double* Mo, int ld) {
+  const int nx = P.nx, ny = P.ny, NN = nx * ny;
+  FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+    const int i = i_, j = j_;
+    auto t = [&](int a, int b) { return T[a * ld + b]; };
+    double v;
+    const bool in_i = i > 0 && i < ny - 1, in_j = j > 0 && j < nx - 1;
+    if (kIn || (in_i && in_j)) {
+      v = t(i, j) + (t(i - 1, j) + t(i + 1, j) + t(i, j - 1) + t(i, j + 1)) / 8 +
+          (t(i - 1, j - 1) + t(i - 1, j + 1) + t(i + 1, j - 1) + t(i + 1, j + 1)) / 16;
+    } else if (in_i && j == nx - 1) {
+      v = (4 * t(i, j) + 2 * t(i - 1, j) + 2 * t(i + 1, j) + 2 * t(i, j - 1) + t(i + 1, j - 1) +
+           t(i - 1, j - 1)) / 12;
+    } else if (in_i && j == 0) {
+      v = (4 * t(i, 0) + 2 * t(i - 1, 0) + 2 * t(i + 1, 0) + 2 * t(i, 1) + t(i + 1, 1) +
+           t(i - 1, 1)) / 12;
+    } else if (in_j && i == ny - 1) {
+      v = (4 * t(i, j) + 2 * t(i, j - 1) + 2 * t(i, j + 1) + 2 * t(i - 1, j) + t(i - 1, j + 1) +
+           t(i - 1, j - 1)) / 12;
+    } else if (in_j && i == 0) {
+      v = (4 * t(0, j) + 2 * t(0, j - 1) + 2 * t(0, j + 1) + 2 * t(1, j) + t(1, j + 1) +
+           t(1, j - 1)) / 12;
+    } else if (i == 0 && j == 0) {
+      v = (4 * t(0, 0) + 2 * t(0, 1) + 2 * t(1, 0) + t(1, 1)) / 9;
+    } else if (i == 0) {  // j == nx-1
+      v = (4 * t(0, j) + 2 * t(0, j - 1) + 2 * t(1, j) + t(1, j - 1)) / 9;
+    } else if (j == 0) {  // i == ny-1
+      v = (4 * t(i, 0) + 2 * t(i, 1) + 2 * t(i - 1, 0) + t(i - 1, 1)) / 9;
+    } else {
+      v = (4 * t(i, j) + 2 * t(i, j - 1) + 2 * t(i - 1, j) + t(i - 1, j - 1)) / 9;
+    }
+    Mo[i * ld + j] = v;
+  });
+}
+
+// Mackenzie regularisation integral sum(mon |J|) dksi deta (:757-759), broadcast to all threads.
+__device__ double monitor_integral(const DropParams& P, const DropMesh& M, const double* T, int ld,
+                                   double* bcast) {
+  const int nx = P.nx, ny = P.ny;
+  double part[1] = {0.0};
+  FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; part[0] += T[i_ * ld + j_] * fabs(M.J[p_]); });
+  const double tot = block_reduce<1, 1, DB>(part);
+  if (threadIdx.x == 0) *bcast = tot * P.dksi * P.deta;
+  __syncthreads();
+  return *bcast;
+}
+
+// Fallback for grids whose working planes do not fit LDS: every field in global (L2) memory.
+__global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, DropMesh M,
+                                                      DropScratch S, double* q, const double* uval,
                                                       const double* uxx0, const double* uyy0,
-                                                      const double* Cx, const double* Cy,
-                                                      const double* den, double dtm, int loops) {
+                                                      PmaTables Tb, double dtm, int loops) {
+  const Coefs& C = Ck;
+  coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   __shared__ double bcast;
   double* uxx = S.A;  // u_xx, u_yy of the current mesh (first iteration: the caller's)
@@ -360,116 +471,243 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs C, Dro
   for (int it = 0; it < loops; ++it) {
     if (it > 0) {
       // compute_Q_spatial_ders, J, compute_u_spatial_ders (:595-597)
-      mesh_stage(P, C, q, M);
+      mesh_stage(P, C, q, nx, M);
       __syncthreads();
-      uders_stage(P, C, M, S, uval);
+      uders_stage(P, C, M, S, uval, nx);
       __syncthreads();
-      lap_pressure_stage(P, C, M, S, uval, uxx, uyy);
-      __syncthreads();
-    }
-    const double* lx = it > 0 ? uxx : uxx0;
-    const double* ly = it > 0 ? uyy : uyy0;
-    // monitor |u_xx + u_yy|^2 (:737), then smoothing_iters passes of the 9-point filter (:740-759)
-    double* T = S.ud;
-    double* Mo = S.ue;
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const double s = fabs(lx[p] + ly[p]);
-      T[p] = s * s;
+      lap_pressure_stage(P, C, M, S, uval, M.A11, M.A22, nx, uxx, uyy, S.ud);
+    } else {
+      FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+        const double s = fabs(uxx0[p_] + uyy0[p_]);  // monitor |u_xx + u_yy|^2 (:737)
+        S.ud[p_] = s * s;
+      });
     }
     __syncthreads();
+    double* T = S.ud;
+    double* Mo = S.ue;
     for (int sm = 0; sm < P.smoothing_iters; ++sm) {
-      for (int p = threadIdx.x; p < NN; p += DB) {
-        const int i = p / nx, j = p - i * nx;
-        auto t = [&](int a, int b) { return T[a * nx + b]; };
-        double v;
-        const bool in_i = i > 0 && i < ny - 1, in_j = j > 0 && j < nx - 1;
-        if (in_i && in_j) {
-          v = t(i, j) + (t(i - 1, j) + t(i + 1, j) + t(i, j - 1) + t(i, j + 1)) / 8 +
-              (t(i - 1, j - 1) + t(i - 1, j + 1) + t(i + 1, j - 1) + t(i + 1, j + 1)) / 16;
-        } else if (in_i && j == nx - 1) {
-          v = (4 * t(i, j) + 2 * t(i - 1, j) + 2 * t(i + 1, j) + 2 * t(i, j - 1) + t(i + 1, j - 1) +
-               t(i - 1, j - 1)) / 12;
-        } else if (in_i && j == 0) {
-          v = (4 * t(i, 0) + 2 * t(i - 1, 0) + 2 * t(i + 1, 0) + 2 * t(i, 1) + t(i + 1, 1) +
-               t(i - 1, 1)) / 12;
-        } else if (in_j && i == ny - 1) {
-          v = (4 * t(i, j) + 2 * t(i, j - 1) + 2 * t(i, j + 1) + 2 * t(i - 1, j) + t(i - 1, j + 1) +
-               t(i - 1, j - 1)) / 12;
-        } else if (in_j && i == 0) {
-          v = (4 * t(0, j) + 2 * t(0, j - 1) + 2 * t(0, j + 1) + 2 * t(1, j) + t(1, j + 1) +
-               t(1, j - 1)) / 12;
-        } else if (i == 0 && j == 0) {
-          v = (4 * t(0, 0) + 2 * t(0, 1) + 2 * t(1, 0) + t(1, 1)) / 9;
-        } else if (i == 0) {  // j == nx-1
-          v = (4 * t(0, j) + 2 * t(0, j - 1) + 2 * t(1, j) + t(1, j - 1)) / 9;
-        } else if (j == 0) {  // i == ny-1
-          v = (4 * t(i, 0) + 2 * t(i, 1) + 2 * t(i - 1, 0) + t(i - 1, 1)) / 9;
-        } else {
-          v = (4 * t(i, j) + 2 * t(i, j - 1) + 2 * t(i - 1, j) + t(i - 1, j - 1)) / 9;
-        }
-        Mo[p] = v;
-      }
+      smooth_pass(P, T, Mo, nx);
       __syncthreads();
       double* sw = T;
       T = Mo;
       Mo = sw;
     }
-    // Mackenzie regularisation: mon += C * sum(mon |J|) dksi deta (:757-759)
-    double part[1] = {0.0};
-    for (int p = threadIdx.x; p < NN; p += DB) part[0] += T[p] * fabs(M.J[p]);
-    const double tot = block_reduce<1, 1, DB>(part);
-    if (threadIdx.x == 0) bcast = tot * P.dksi * P.deta;
-    __syncthreads();
-    const double integral = bcast;
+    const double integral = monitor_integral(P, M, T, nx, &bcast);
     // q_rhs = sqrt(mon |J|) / alpha (:584)
     double* X = S.p;
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const double mon = T[p] + P.C * integral;
-      X[p] = sqrt(mon * fabs(M.J[p])) / P.alpha;
-    }
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; X[p_] = sqrt((T[p_] + P.C * integral) * fabs(M.J[p_])) / P.alpha; });
     __syncthreads();
     // 2-D DCT-II ortho: T1 = Cy X (along eta), T2 = T1 Cx^T (along xi) (:585)
     double* T1 = S.t1;
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const int k = p / nx, j = p - k * nx;
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+      const int k = i_, j = j_;
       double acc = 0.0;
-      for (int i = 0; i < ny; ++i) acc += Cy[k * ny + i] * X[i * nx + j];
-      T1[p] = acc;
-    }
+      for (int i = 0; i < ny; ++i) acc += Tb.cy[k * ny + i] * X[i * nx + j];
+      T1[p_] = acc;
+    });
     __syncthreads();
     double* T2 = S.t2;
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const int k = p / nx, l = p - k * nx;
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+      const int k = i_, l = j_;
       double acc = 0.0;
-      for (int j = 0; j < nx; ++j) acc += T1[k * nx + j] * Cx[l * nx + j];
-      T2[p] = acc / den[p];  // / (1 - gamma Leig) (:586)
-    }
+      for (int j = 0; j < nx; ++j) acc += T1[k * nx + j] * Tb.cx[l * nx + j];
+      T2[p_] = acc / Tb.den[p_];  // / (1 - gamma Leig) (:586)
+    });
     __syncthreads();
     // inverse (DCT-III ortho): Y1 = Cy^T T2, dQ = Y1 Cx (:586-587)
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const int i = p / nx, l = p - i * nx;
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+      const int i = i_, l = j_;
       double acc = 0.0;
-      for (int k = 0; k < ny; ++k) acc += Cy[k * ny + i] * T2[k * nx + l];
-      T1[p] = acc;
-    }
+      for (int k = 0; k < ny; ++k) acc += Tb.cy[k * ny + i] * T2[k * nx + l];
+      T1[p_] = acc;
+    });
     __syncthreads();
-    for (int p = threadIdx.x; p < NN; p += DB) {
-      const int i = p / nx, j = p - i * nx;
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+      const int i = i_, j = j_;
       double acc = 0.0;
-      for (int l = 0; l < nx; ++l) acc += T1[i * nx + l] * Cx[l * nx + j];
-      q[p] = q[p] + dtm * acc;  // Q.val += dt * Q.dt (:591, :599)
-    }
+      for (int l = 0; l < nx; ++l) acc += T1[i * nx + l] * Tb.cx[l * nx + j];
+      q[p_] = q[p_] + dtm * acc;  // Q.val += dt * Q.dt (:591, :599)
+    });
     __syncthreads();
   }
 }
 
+// ---- LDS-resident variant.  Three LDS planes (row stride ld = nx|1, odd so that column walks
+// are bank-conflict free) hold the stencil inputs of each stage and the DCT intermediates.  The
+// DCT products put the constant matrix on the WAVE-UNIFORM side: a wave owns kTile output rows
+// (or columns), so the matrix entries arrive through scalar loads (one fetch per wave, not 64
+// lane copies through the LDS return path) while each lane streams its LDS operand.
+constexpr int kTile = 8;
+constexpr int kWaves = DB / 64;
+
+// out(m, n) = sum_{r<K} A(m, r) B(r, n): wave-uniform A rows m0..m0+kTile-1 read as
+// At[r*lda + m] (global, padded), lanes over n with B[r*ld + n] in LDS.
+template <class Fn>
+__device__ __forceinline__ void dct_rows(const double* __restrict__ At, int lda, const double* B,
+                                         int ld, int K, int M, int N, Fn f) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nc = (N + 63) >> 6, ntask = ((M + kTile - 1) / kTile) * nc;
+  for (int task = wave; task < ntask; task += kWaves) {
+    const int m0 = (task / nc) * kTile, n = (task % nc) * 64 + lane;
+    const double* b = B + min(n, N - 1);
+    const double* a = At + m0;
+    double acc[kTile];
+#pragma unroll
+    for (int t = 0; t < kTile; ++t) acc[t] = 0.0;
+#pragma unroll 2
+    for (int r = 0; r < K; ++r) {
+      const double bv = b[r * ld];
+#pragma unroll
+      for (int t = 0; t < kTile; ++t) acc[t] = fma(a[r * lda + t], bv, acc[t]);
+    }
+    if (n < N) {
+#pragma unroll
+      for (int t = 0; t < kTile; ++t)
+        if (m0 + t < M) f(m0 + t, n, acc[t]);
+    }
+  }
+}
+
+// out(m, n) = sum_{r<K} A(m, r) B(r, n): wave-uniform B columns n0..n0+kTile-1 read as
+// Bt[r*ldb + n] (global, padded), lanes over m with A[m*ld + r] in LDS.
+template <class Fn>
+__device__ __forceinline__ void dct_cols(const double* A, int ld, const double* __restrict__ Bt,
+                                         int ldb, int K, int M, int N, Fn f) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int mc = (M + 63) >> 6, ntask = ((N + kTile - 1) / kTile) * mc;
+  for (int task = wave; task < ntask; task += kWaves) {
+    const int n0 = (task / mc) * kTile, m = (task % mc) * 64 + lane;
+    const double* a = A + min(m, M - 1) * ld;
+    const double* b = Bt + n0;
+    double acc[kTile];
+#pragma unroll
+    for (int t = 0; t < kTile; ++t) acc[t] = 0.0;
+#pragma unroll 2
+    for (int r = 0; r < K; ++r) {
+      const double av = a[r];
+#pragma unroll
+      for (int t = 0; t < kTile; ++t) acc[t] = fma(av, b[r * ldb + t], acc[t]);
+    }
+    if (m < M) {
+#pragma unroll
+      for (int t = 0; t < kTile; ++t)
+        if (n0 + t < N) f(m, n0 + t, acc[t]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
+    DropParams P, Coefs Ck, DropMesh M, DropScratch S, double* q, const double* uval,
+    const double* uxx0, const double* uyy0, const double* __restrict__ cx,
+    const double* __restrict__ cxt, const double* __restrict__ cy, const double* __restrict__ cyt,
+    const double* __restrict__ den, double dtm, int loops, unsigned long long* tprof) {
+  const Coefs& C = Ck;
+  coef_rows_init(C);
+  const int nx = P.nx, ny = P.ny, NN = nx * ny, ld = nx | 1;
+  __shared__ double bcast;
+  extern __shared__ double lds[];
+  double* L0 = lds;
+  double* L1 = L0 + ny * ld;
+  double* L2 = L1 + ny * ld;
+  // optional per-stage timing (NKHIP_PMA_TIMING): thread 0 accumulates wall-clock deltas
+  unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = 0;
+  auto mark = [&](int k) {
+    if (tprof && threadIdx.x == 0) {
+      const unsigned long long t = wall_clock64();
+      if (k >= 0) tacc[k] += t - tlast;
+      tlast = t;
+    }
+  };
+  mark(-1);
+  for (int it = 0; it < loops; ++it) {
+    if (it > 0) {
+      // compute_Q_spatial_ders + J (:595-596) from q staged in L0; A11 -> L1, A22 -> L2
+      FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = q[p_]; });
+      __syncthreads();
+      mesh_stage(P, C, L0, ld, M, L1, L2);
+      __syncthreads();
+      mark(0);
+      // compute_u_spatial_ders (:597) from u staged in L0
+      FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = uval[p_]; });
+      __syncthreads();
+      uders_stage(P, C, M, S, L0, ld);
+      __syncthreads();
+      lap_pressure_stage(P, C, M, S, L0, L1, L2, ld, S.A, S.B, S.ud);
+      __syncthreads();
+      FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = S.ud[p_]; });
+      mark(1);
+    } else {
+      FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+        const double s = fabs(uxx0[p_] + uyy0[p_]);  // monitor |u_xx + u_yy|^2 (:737)
+        L0[i_ * ld + j_] = s * s;
+      });
+    }
+    __syncthreads();
+    double* T = L0;
+    double* Mo = L1;
+    for (int sm = 0; sm < P.smoothing_iters; ++sm) {
+      smooth_pass(P, T, Mo, ld);
+      __syncthreads();
+      double* sw = T;
+      T = Mo;
+      Mo = sw;
+    }
+    mark(2);
+    const double integral = monitor_integral(P, M, T, ld, &bcast);
+    // q_rhs = sqrt(mon |J|) / alpha (:584) -> L2
+    FOR_POINTS(NN) {
+    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
+      L2[i_ * ld + j_] = sqrt((T[i_ * ld + j_] + P.C * integral) * fabs(M.J[p_])) / P.alpha;
+    });
+    __syncthreads();
+    mark(3);
+    // DCT-II along eta: T1 = Cy X (L2 -> L0)
+    dct_rows(cyt, ny, L2, ld, ny, ny, nx, [&](int m, int n, double v) { L0[m * ld + n] = v; });
+    __syncthreads();
+    // along xi: T2 = T1 Cx^T, / (1 - gamma Leig) (:585-586) (L0 -> L1)
+    dct_cols(L0, ld, cxt, nx, nx, ny, nx,
+             [&](int m, int n, double v) { L1[m * ld + n] = v / den[m * nx + n]; });
+    __syncthreads();
+    // inverse (DCT-III ortho) along eta: Y1 = Cy^T T2 (L1 -> L2)
+    dct_rows(cy, ny, L1, ld, ny, ny, nx, [&](int m, int n, double v) { L2[m * ld + n] = v; });
+    __syncthreads();
+    // along xi: dQ = Y1 Cx; Q.val += dt * Q.dt (:587, :591, :599)
+    dct_cols(L2, ld, cx, nx, nx, ny, nx,
+             [&](int m, int n, double v) { q[m * nx + n] = q[m * nx + n] + dtm * v; });
+    __syncthreads();
+    mark(4);
+  }
+  if (tprof && threadIdx.x == 0)
+    for (int k = 0; k < 5; ++k) tprof[k] = tacc[k];
+}
+
 
 Coefs make_coefs(const DropParams& P) {
-  Coefs C;
-  C.d1x = make_d1(P.dksi);
-  C.d1y = make_d1(P.deta);
-  C.d2x = make_d2(P.dksi * P.dksi);
-  C.d2y = make_d2(P.deta * P.deta);
+  // make_M's weights (:782-806): interior rows {1,-8,0,8,-1}/12h and {-1,16,-30,16,-1}/12h^2
+  Coefs C{};
+  const double d1[5] = {1, -8, 0, 8, -1}, d2[5] = {-1, 16, -30, 16, -1};
+  C.s[0] = 12 * P.dksi;
+  C.s[1] = 12 * P.deta;
+  C.s[2] = 12 * (P.dksi * P.dksi);
+  C.s[3] = 12 * (P.deta * P.deta);
+  for (int k = 0; k < 5; ++k) {
+    C.in[0][k] = d1[k] / C.s[0];
+    C.in[1][k] = d1[k] / C.s[1];
+    C.in[2][k] = d2[k] / C.s[2];
+    C.in[3][k] = d2[k] / C.s[3];
+  }
   return C;
 }
 
@@ -502,36 +740,82 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
 }
 
 // Host side: DCT matrices and the (1 - gamma Leig) divisor, uploaded once per stepper.
-void drop_pma_tables(const DropParams& P, std::vector<double>* cx, std::vector<double>* cy,
-                     std::vector<double>* den) {
-  auto dct = [](int n, std::vector<double>* c) {
-    c->assign(size_t(n) * n, 0.0);
+size_t drop_pma_table_size(const DropParams& P) {
+  return 2 * (size_t(P.nx) * P.nx + kPmaPad) + 2 * (size_t(P.ny) * P.ny + kPmaPad) +
+         size_t(P.nx) * P.ny;
+}
+
+PmaTables drop_pma_view(const DropParams& P, const double* t) {
+  PmaTables T;
+  const size_t sx = size_t(P.nx) * P.nx + kPmaPad, sy = size_t(P.ny) * P.ny + kPmaPad;
+  T.cx = t;
+  T.cxt = t + sx;
+  T.cy = t + 2 * sx;
+  T.cyt = T.cy + sy;
+  T.den = T.cyt + sy;
+  return T;
+}
+
+std::vector<double> drop_pma_tables(const DropParams& P) {
+  std::vector<double> out(drop_pma_table_size(P), 0.0);
+  const PmaTables T = drop_pma_view(P, out.data());
+  auto dct = [](int n, double* c, double* ct) {
     for (int k = 0; k < n; ++k)
-      for (int m = 0; m < n; ++m)
-        (*c)[size_t(k) * n + m] =
+      for (int m = 0; m < n; ++m) {
+        const double v =
             std::sqrt((k == 0 ? 1.0 : 2.0) / n) * std::cos(M_PI * k * (2 * m + 1) / (2.0 * n));
+        c[size_t(k) * n + m] = v;
+        ct[size_t(m) * n + k] = v;
+      }
   };
-  dct(P.nx, cx);
-  dct(P.ny, cy);
-  den->assign(size_t(P.nx) * P.ny, 0.0);
+  dct(P.nx, const_cast<double*>(T.cx), const_cast<double*>(T.cxt));
+  dct(P.ny, const_cast<double*>(T.cy), const_cast<double*>(T.cyt));
+  double* den = const_cast<double*>(T.den);
   for (int i = 0; i < P.ny; ++i)
     for (int j = 0; j < P.nx; ++j) {
       // M.Leig (:829-833), including the division by dksi*deta
       const double a = 2 * std::cos(M_PI * i / (P.ny - 1)) - 2;
       const double b = 2 * std::cos(M_PI * j / (P.nx - 1)) - 2;
       const double leig = (a * 1.0 + 1.0 * b) / (P.dksi * P.deta);
-      (*den)[size_t(i) * P.nx + j] = 1 - P.gamma * leig;
+      den[size_t(i) * P.nx + j] = 1 - P.gamma * leig;
     }
+  return out;
 }
 
 hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, double* q,
                            const double* uval, const double* uxx0, const double* uyy0,
-                           const double* Cx, const double* Cy, const double* den, double dtm,
-                           int loops, hipStream_t s) {
-  if (P.nx < 7 || P.ny < 7 || loops < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(drop_pma_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, q, uval, uxx0,
-                     uyy0, Cx, Cy, den, dtm, loops);
-  return hipGetLastError();
+                           const PmaTables& T, double dtm, int loops, hipStream_t s) {
+  if (!shape_ok(P) || loops < 1) return hipErrorInvalidValue;
+  static unsigned long long* tprof = [] {
+    unsigned long long* t = nullptr;
+    if (env_flag("NKHIP_PMA_TIMING") && hipMalloc(&t, 64) != hipSuccess) t = nullptr;
+    return t;
+  }();
+  const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
+  static const bool force_global = env_flag("NKHIP_PMA_GLOBAL") != 0;
+  if (!force_global && lds <= kPmaLdsMax) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&drop_pma_lds_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(drop_pma_lds_kernel, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S, q,
+                       uval, uxx0, uyy0, T.cx, T.cxt, T.cy, T.cyt, T.den, dtm, loops, tprof);
+  } else {
+    hipLaunchKernelGGL(drop_pma_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, q, uval,
+                       uxx0, uyy0, T, dtm, loops);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess && tprof && !force_global) {
+    // debug: per-stage wall-clock (100 MHz) of this launch, to stderr
+    unsigned long long h[5];
+    if (hipMemcpyAsync(h, tprof, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess)
+      std::fprintf(stderr,
+                   "pma us/loop: mesh %.2f uders+lap %.2f smooth %.2f rhs %.2f dct %.2f\n",
+                   h[0] / 100.0 / loops, h[1] / 100.0 / loops, h[2] / 100.0 / loops,
+                   h[3] / 100.0 / loops, h[4] / 100.0 / loops);
+  }
+  return e;
 }
 
 }  // namespace nk

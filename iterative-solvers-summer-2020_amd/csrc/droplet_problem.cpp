@@ -96,25 +96,19 @@ DropletStepper::DropletStepper(const DropParams& Pp, const nk_opts& o, hipStream
     status_ = NK_->status();
     return;
   }
-  std::vector<double> cx, cy, den;
-  drop_pma_tables(Pp, &cx, &cy, &den);
-  if (hipMalloc(reinterpret_cast<void**>(&cx_), sizeof(double) * (cx.size() + cy.size() + den.size())) !=
-      hipSuccess) {
-    cx_ = nullptr;
+  const std::vector<double> tab = drop_pma_tables(Pp);
+  if (hipMalloc(reinterpret_cast<void**>(&tables_), sizeof(double) * tab.size()) != hipSuccess) {
+    tables_ = nullptr;
     status_ = NK_ENOMEM;
     return;
   }
-  cy_ = cx_ + cx.size();
-  den_ = cy_ + cy.size();
-  hipMemcpyAsync(cx_, cx.data(), sizeof(double) * cx.size(), hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(cy_, cy.data(), sizeof(double) * cy.size(), hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(den_, den.data(), sizeof(double) * den.size(), hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(tables_, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice, s);
   status_ = E.sync();
 }
 
 DropletStepper::~DropletStepper() {
   if (E.s) hipStreamSynchronize(E.s);
-  if (cx_) hipFree(cx_);
+  if (tables_) hipFree(tables_);
 }
 
 int DropletStepper::set_state(const double* U, const double* Q) {
@@ -146,8 +140,8 @@ int DropletStepper::solve(double dt, double* U, nk_stats* st) {
 int DropletStepper::pma(double dtm, int loops) {
   const DropParams& Pp = P.params();
   return E.launch(K_USERF, 0.0, [&] {
-    return drop_pma_launch(Pp, P.mesh(), P.scratch(), P.qval, P.uval, P.uxx, P.uyy, cx_, cy_,
-                           den_, dtm, loops, E.s);
+    return drop_pma_launch(Pp, P.mesh(), P.scratch(), P.qval, P.uval, P.uxx, P.uyy,
+                           drop_pma_view(Pp, tables_), dtm, loops, E.s);
   });
 }
 

@@ -61,7 +61,7 @@ class DropletStepper {
 
  private:
   std::unique_ptr<NewtonKrylov> NK_;
-  double *cx_ = nullptr, *cy_ = nullptr, *den_ = nullptr;
+  double* tables_ = nullptr;  // PMA DCT tables (drop_pma_tables)
   int status_ = NK_OK;
 };
 
