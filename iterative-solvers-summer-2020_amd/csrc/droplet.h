@@ -57,12 +57,15 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              double* xt, double* partial, hipStream_t s);
 
 // Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
-// Cy (ny*ny), their transposes, and den = 1 - gamma*Leig (ny*nx).  Packed in one allocation of
-// drop_pma_table_size() doubles, each matrix followed by kPmaPad zeros (tile over-reads).
+// Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the four DCT operands of the MFMA path in
+// v_mfma_f64_16x16x4 fragment order (zero-padded to 16-row/column tiles and 4-deep k steps):
+//   fa1: A = Cy     (T1 = Cy X)      fb2: B = Cx^T (T2 = T1 Cx^T)
+//   fa3: A = Cy^T   (Y1 = Cy^T T2)   fb4: B = Cx   (dQ = Y1 Cx)
+// A fragments: [mt][s][lane] = A[16mt + (lane&15)][4s + (lane>>4)];
+// B fragments: [nt][s][lane] = B[4s + (lane>>4)][16nt + (lane&15)].
 struct PmaTables {
-  const double *cx, *cxt, *cy, *cyt, *den;
+  const double *cx, *cy, *den, *fa1, *fb2, *fa3, *fb4;
 };
-constexpr int kPmaPad = 8;
 size_t drop_pma_table_size(const DropParams& P);
 std::vector<double> drop_pma_tables(const DropParams& P);
 PmaTables drop_pma_view(const DropParams& P, const double* packed);

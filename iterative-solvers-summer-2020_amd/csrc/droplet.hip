@@ -540,74 +540,77 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
 
 // ---- LDS-resident variant.  Three LDS planes (row stride ld = nx|1, odd so that column walks
 // are bank-conflict free) hold the stencil inputs of each stage and the DCT intermediates.  The
-// DCT products put the constant matrix on the WAVE-UNIFORM side: a wave owns kTile output rows
-// (or columns), so the matrix entries arrive through scalar loads (one fetch per wave, not 64
-// lane copies through the LDS return path) while each lane streams its LDS operand.
-constexpr int kTile = 8;
+// four DCT products run on v_mfma_f64_16x16x4: the constant DCT operand streams from a global
+// table already in fragment order (one coalesced 512-B load per wave and k step), the data
+// operand comes from the LDS plane; one lane operand pair feeds 256 multiply-adds.
 constexpr int kWaves = DB / 64;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kBatch = 4;  // k steps whose operands load together
 
-// out(m, n) = sum_{r<K} A(m, r) B(r, n): wave-uniform A rows m0..m0+kTile-1 read as
-// At[r*lda + m] (global, padded), lanes over n with B[r*ld + n] in LDS.
-template <class Fn>
-__device__ __forceinline__ void dct_rows(const double* __restrict__ At, int lda, const double* B,
-                                         int ld, int K, int M, int N, Fn f) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int nc = (N + 63) >> 6, ntask = ((M + kTile - 1) / kTile) * nc;
-  for (int task = wave; task < ntask; task += kWaves) {
-    const int m0 = (task / nc) * kTile, n = (task % nc) * 64 + lane;
-    const double* b = B + min(n, N - 1);
-    const double* a = At + m0;
-    double acc[kTile];
-#pragma unroll
-    for (int t = 0; t < kTile; ++t) acc[t] = 0.0;
-#pragma unroll 2
-    for (int r = 0; r < K; ++r) {
-      const double bv = b[r * ld];
-#pragma unroll
-      for (int t = 0; t < kTile; ++t) acc[t] = fma(a[r * lda + t], bv, acc[t]);
-    }
-    if (n < N) {
-#pragma unroll
-      for (int t = 0; t < kTile; ++t)
-        if (m0 + t < M) f(m0 + t, n, acc[t]);
-    }
-  }
+// k steps of a K-deep product, padded to a multiple of kBatch (the tables hold zeros there)
+__host__ __device__ inline int pma_ksteps(int K) { return ((K + 3) / 4 + kBatch - 1) / kBatch * kBatch; }
+
+__device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// out(m, n) = sum_{r<K} A(m, r) B(r, n): wave-uniform B columns n0..n0+kTile-1 read as
-// Bt[r*ldb + n] (global, padded), lanes over m with A[m*ld + r] in LDS.
-template <class Fn>
-__device__ __forceinline__ void dct_cols(const double* A, int ld, const double* __restrict__ Bt,
-                                         int ldb, int K, int M, int N, Fn f) {
+// out(m, n) = sum_{k<K} A(m, k) B(k, n), m < M, n < N.
+// kConstA: A from fragment table `frag`, B(k, n) = plane[k*ld + n]; a wave task is 16 x 32.
+// else:    B from fragment table `frag`, A(m, k) = plane[m*ld + k]; a wave task is 32 x 16.
+// Padded k (>= K) has zero fragment entries; the plane index is clamped so it reads finite data.
+template <bool kConstA, class Fn>
+__device__ __forceinline__ void dct_mfma(const double* __restrict__ frag, const double* plane,
+                                         int ld, int K, int M, int N, Fn f) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int mc = (M + 63) >> 6, ntask = ((N + kTile - 1) / kTile) * mc;
-  for (int task = wave; task < ntask; task += kWaves) {
-    const int n0 = (task / mc) * kTile, m = (task % mc) * 64 + lane;
-    const double* a = A + min(m, M - 1) * ld;
-    const double* b = Bt + n0;
-    double acc[kTile];
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int S = pma_ksteps(K), Mt = (M + 15) >> 4, Nt = (N + 15) >> 4;
+  const int tM = kConstA ? Mt : (Mt + 1) >> 1, tN = kConstA ? (Nt + 1) >> 1 : Nt;
+  for (int task = wave; task < tM * tN; task += kWaves) {
+    const int ti = task / tN, tj = task - ti * tN;
+    // tile origins: two tiles side by side (kConstA: along n; else along m)
+    const int m0 = kConstA ? 16 * ti : 32 * ti, n0 = kConstA ? 32 * tj : 16 * tj;
+    const double* fr = frag + size_t(kConstA ? ti : tj) * S * 64 + lane;
+    f64x4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = {0.0, 0.0, 0.0, 0.0};
+    // operands of kBatch k steps are loaded together, then their MFMAs issue: one memory
+    // round trip per batch instead of per step (steps past S are skipped, uniformly)
+    const double* p0 = kConstA ? plane + min(n0 + r, N - 1) : plane + min(m0 + r, M - 1) * ld;
+    const double* p1 =
+        kConstA ? plane + min(n0 + 16 + r, N - 1) : plane + min(m0 + 16 + r, M - 1) * ld;
+    const int kstride = kConstA ? ld : 1;
+    for (int s0 = 0; s0 < S; s0 += kBatch) {  // S is a multiple of kBatch (zero-padded)
+      double fv[kBatch], x0[kBatch], x1[kBatch];
 #pragma unroll
-    for (int t = 0; t < kTile; ++t) acc[t] = 0.0;
-#pragma unroll 2
-    for (int r = 0; r < K; ++r) {
-      const double av = a[r];
+      for (int u = 0; u < kBatch; ++u) {
+        const int k = min(4 * (s0 + u) + g, K - 1);
+        fv[u] = fr[(s0 + u) * 64];
+        x0[u] = p0[k * kstride];
+        x1[u] = p1[k * kstride];
+      }
 #pragma unroll
-      for (int t = 0; t < kTile; ++t) acc[t] = fma(av, b[r * ldb + t], acc[t]);
+      for (int u = 0; u < kBatch; ++u) {
+        c0 = kConstA ? mfma_f64(fv[u], x0[u], c0) : mfma_f64(x0[u], fv[u], c0);
+        c1 = kConstA ? mfma_f64(fv[u], x1[u], c1) : mfma_f64(x1[u], fv[u], c1);
+      }
     }
-    if (m < M) {
+    // D layout: row = (lane >> 4) + 4*reg, col = lane & 15
 #pragma unroll
-      for (int t = 0; t < kTile; ++t)
-        if (n0 + t < N) f(m, n0 + t, acc[t]);
+    for (int v = 0; v < 4; ++v) {
+      const int m = m0 + g + 4 * v, n = n0 + r;
+      if (kConstA) {
+        if (m < M && n < N) f(m, n, c0[v]);
+        if (m < M && n + 16 < N) f(m, n + 16, c1[v]);
+      } else {
+        if (m < M && n < N) f(m, n, c0[v]);
+        if (m + 16 < M && n < N) f(m + 16, n, c1[v]);
+      }
     }
   }
 }
 
 __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
     DropParams P, Coefs Ck, DropMesh M, DropScratch S, double* q, const double* uval,
-    const double* uxx0, const double* uyy0, const double* __restrict__ cx,
-    const double* __restrict__ cxt, const double* __restrict__ cy, const double* __restrict__ cyt,
+    const double* uxx0, const double* uyy0, const double* __restrict__ fa1,
+    const double* __restrict__ fb2, const double* __restrict__ fa3, const double* __restrict__ fb4,
     const double* __restrict__ den, double dtm, int loops, unsigned long long* tprof) {
   const Coefs& C = Ck;
   coef_rows_init(C);
@@ -674,18 +677,18 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
     __syncthreads();
     mark(3);
     // DCT-II along eta: T1 = Cy X (L2 -> L0)
-    dct_rows(cyt, ny, L2, ld, ny, ny, nx, [&](int m, int n, double v) { L0[m * ld + n] = v; });
+    dct_mfma<true>(fa1, L2, ld, ny, ny, nx, [&](int m, int n, double v) { L0[m * ld + n] = v; });
     __syncthreads();
     // along xi: T2 = T1 Cx^T, / (1 - gamma Leig) (:585-586) (L0 -> L1)
-    dct_cols(L0, ld, cxt, nx, nx, ny, nx,
-             [&](int m, int n, double v) { L1[m * ld + n] = v / den[m * nx + n]; });
+    dct_mfma<false>(fb2, L0, ld, nx, ny, nx,
+                    [&](int m, int n, double v) { L1[m * ld + n] = v / den[m * nx + n]; });
     __syncthreads();
     // inverse (DCT-III ortho) along eta: Y1 = Cy^T T2 (L1 -> L2)
-    dct_rows(cy, ny, L1, ld, ny, ny, nx, [&](int m, int n, double v) { L2[m * ld + n] = v; });
+    dct_mfma<true>(fa3, L1, ld, ny, ny, nx, [&](int m, int n, double v) { L2[m * ld + n] = v; });
     __syncthreads();
     // along xi: dQ = Y1 Cx; Q.val += dt * Q.dt (:587, :591, :599)
-    dct_cols(L2, ld, cx, nx, nx, ny, nx,
-             [&](int m, int n, double v) { q[m * nx + n] = q[m * nx + n] + dtm * v; });
+    dct_mfma<false>(fb4, L2, ld, nx, ny, nx,
+                    [&](int m, int n, double v) { q[m * nx + n] = q[m * nx + n] + dtm * v; });
     __syncthreads();
     mark(4);
   }
@@ -739,46 +742,78 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
   return hipGetLastError();
 }
 
-// Host side: DCT matrices and the (1 - gamma Leig) divisor, uploaded once per stepper.
+// Host side: DCT matrices, the (1 - gamma Leig) divisor and the MFMA fragment tables, uploaded
+// once per stepper.
+namespace {
+size_t frag_size(int tiles, int K) { return size_t(tiles) * pma_ksteps(K) * 64; }
+}  // namespace
+
 size_t drop_pma_table_size(const DropParams& P) {
-  return 2 * (size_t(P.nx) * P.nx + kPmaPad) + 2 * (size_t(P.ny) * P.ny + kPmaPad) +
-         size_t(P.nx) * P.ny;
+  const int mt = (P.ny + 15) / 16, nt = (P.nx + 15) / 16;
+  return size_t(P.nx) * P.nx + size_t(P.ny) * P.ny + size_t(P.nx) * P.ny +
+         2 * frag_size(mt, P.ny) + 2 * frag_size(nt, P.nx);
 }
 
 PmaTables drop_pma_view(const DropParams& P, const double* t) {
+  const int mt = (P.ny + 15) / 16, nt = (P.nx + 15) / 16;
   PmaTables T;
-  const size_t sx = size_t(P.nx) * P.nx + kPmaPad, sy = size_t(P.ny) * P.ny + kPmaPad;
   T.cx = t;
-  T.cxt = t + sx;
-  T.cy = t + 2 * sx;
-  T.cyt = T.cy + sy;
-  T.den = T.cyt + sy;
+  T.cy = T.cx + size_t(P.nx) * P.nx;
+  T.den = T.cy + size_t(P.ny) * P.ny;
+  T.fa1 = T.den + size_t(P.nx) * P.ny;
+  T.fb2 = T.fa1 + frag_size(mt, P.ny);
+  T.fa3 = T.fb2 + frag_size(nt, P.nx);
+  T.fb4 = T.fa3 + frag_size(mt, P.ny);
   return T;
 }
 
 std::vector<double> drop_pma_tables(const DropParams& P) {
   std::vector<double> out(drop_pma_table_size(P), 0.0);
   const PmaTables T = drop_pma_view(P, out.data());
-  auto dct = [](int n, double* c, double* ct) {
+  auto W = [](const double* p) { return const_cast<double*>(p); };
+  auto dct = [](int n, double* c) {
     for (int k = 0; k < n; ++k)
-      for (int m = 0; m < n; ++m) {
-        const double v =
+      for (int m = 0; m < n; ++m)
+        c[size_t(k) * n + m] =
             std::sqrt((k == 0 ? 1.0 : 2.0) / n) * std::cos(M_PI * k * (2 * m + 1) / (2.0 * n));
-        c[size_t(k) * n + m] = v;
-        ct[size_t(m) * n + k] = v;
-      }
   };
-  dct(P.nx, const_cast<double*>(T.cx), const_cast<double*>(T.cxt));
-  dct(P.ny, const_cast<double*>(T.cy), const_cast<double*>(T.cyt));
-  double* den = const_cast<double*>(T.den);
-  for (int i = 0; i < P.ny; ++i)
-    for (int j = 0; j < P.nx; ++j) {
+  const int nx = P.nx, ny = P.ny;
+  dct(nx, W(T.cx));
+  dct(ny, W(T.cy));
+  double* den = W(T.den);
+  for (int i = 0; i < ny; ++i)
+    for (int j = 0; j < nx; ++j) {
       // M.Leig (:829-833), including the division by dksi*deta
-      const double a = 2 * std::cos(M_PI * i / (P.ny - 1)) - 2;
-      const double b = 2 * std::cos(M_PI * j / (P.nx - 1)) - 2;
+      const double a = 2 * std::cos(M_PI * i / (ny - 1)) - 2;
+      const double b = 2 * std::cos(M_PI * j / (nx - 1)) - 2;
       const double leig = (a * 1.0 + 1.0 * b) / (P.dksi * P.deta);
-      den[size_t(i) * P.nx + j] = 1 - P.gamma * leig;
+      den[size_t(i) * nx + j] = 1 - P.gamma * leig;
     }
+  // fragment tables; A(m, k) / B(k, n) accessors with zero padding
+  auto fill_a = [](double* f, int M, int K, auto A) {
+    const int S = pma_ksteps(K);
+    for (int mt = 0; mt < (M + 15) / 16; ++mt)
+      for (int s = 0; s < S; ++s)
+        for (int l = 0; l < 64; ++l) {
+          const int m = 16 * mt + (l & 15), k = 4 * s + (l >> 4);
+          f[(size_t(mt) * S + s) * 64 + l] = (m < M && k < K) ? A(m, k) : 0.0;
+        }
+  };
+  auto fill_b = [](double* f, int K, int N, auto B) {
+    const int S = pma_ksteps(K);
+    for (int nt = 0; nt < (N + 15) / 16; ++nt)
+      for (int s = 0; s < S; ++s)
+        for (int l = 0; l < 64; ++l) {
+          const int k = 4 * s + (l >> 4), n = 16 * nt + (l & 15);
+          f[(size_t(nt) * S + s) * 64 + l] = (k < K && n < N) ? B(k, n) : 0.0;
+        }
+  };
+  const double* cx = T.cx;
+  const double* cy = T.cy;
+  fill_a(W(T.fa1), ny, ny, [&](int m, int k) { return cy[size_t(m) * ny + k]; });
+  fill_b(W(T.fb2), nx, nx, [&](int k, int n) { return cx[size_t(n) * nx + k]; });
+  fill_a(W(T.fa3), ny, ny, [&](int m, int k) { return cy[size_t(k) * ny + m]; });
+  fill_b(W(T.fb4), nx, nx, [&](int k, int n) { return cx[size_t(k) * nx + n]; });
   return out;
 }
 
@@ -799,7 +834,7 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(drop_pma_lds_kernel, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S, q,
-                       uval, uxx0, uyy0, T.cx, T.cxt, T.cy, T.cyt, T.den, dtm, loops, tprof);
+                       uval, uxx0, uyy0, T.fa1, T.fb2, T.fa3, T.fb4, T.den, dtm, loops, tprof);
   } else {
     hipLaunchKernelGGL(drop_pma_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, q, uval,
                        uxx0, uyy0, T, dtm, loops);
