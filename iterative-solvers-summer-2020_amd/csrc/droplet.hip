@@ -126,10 +126,10 @@ __device__ __forceinline__ double dxy(const Coefs& C, const double* v, int i, in
 // The explicit part of Laplace_operator along one axis (:616-668): v_xx (axis = x, A = A11) or
 // v_yy (axis = y, A = A22) at position `pos` of a line of length n, element k at v[k*stride].
 template <bool kIn = false>
-__device__ __forceinline__ double lap_axis(const double* v, const double* A, int pos, int n,
-                                           int s, double h2) {
-  auto V = [&](int k) { return v[k * s]; };
-  auto a = [&](int k) { return A[k * s]; };
+__device__ __forceinline__ double lap_axis(const double* v, int sv, const double* A, int sa,
+                                           int pos, int n, double h2) {
+  auto V = [&](int k) { return v[k * sv]; };
+  auto a = [&](int k) { return A[k * sa]; };
   const int m = pos;
   if (kIn || (m >= 3 && m <= n - 4)) {  // interior (:617-631)
     return (4 * (a(m - 1) * (V(m - 3) - 8 * V(m - 2) + 8 * V(m) - V(m + 1)))
@@ -255,43 +255,67 @@ __global__ void __launch_bounds__(DB) drop_mesh_kernel(DropParams P, Coefs Ck, c
   mesh_stage(P, C, q, P.nx, M);
 }
 
+// A row-major field with row stride ld: global fields use nx, LDS planes nx|1.
+struct Plane {
+  double* v;
+  int ld;
+  __device__ double& operator()(int i, int j) const { return v[i * ld + j]; }
+};
+struct CPlane {
+  const double* v;
+  int ld;
+  __device__ CPlane(const double* v_, int ld_) : v(v_), ld(ld_) {}
+  __device__ CPlane(const Plane& p) : v(p.v), ld(p.ld) {}
+  __device__ double operator()(int i, int j) const { return v[i * ld + j]; }
+};
+
+template <bool kIn>
+__device__ __forceinline__ double dx1(const Coefs& C, CPlane f, int i, int j, int nx) {
+  return dx1<kIn>(C, f.v, i, j, nx, f.ld);
+}
+template <bool kIn>
+__device__ __forceinline__ double dy1(const Coefs& C, CPlane f, int i, int j, int ny) {
+  return dy1<kIn>(C, f.v, i, j, ny, f.ld);
+}
+
 // compute_u_spatial_ders (:713-727) first half: u_xi, u_eta with its boundary rules, incl. the
 // U_dksi[Bottom] quirk (:722), as the cross-term inputs t1 = A12 u_eta, t2 = A12 u_xi.
-__device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                            const DropScratch& S, const double* u, int ldu) {
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_, i = i_, j = j_;
-    double ud = dx1<kIn>(C, u, i, j, nx, ldu), ue = dy1<kIn>(C, u, i, j, ny, ldu);
-    if (j == 0 || j == nx - 1) ud = 0.0;
-    if (i == ny - 1) ue = 0.0;
-    if (i == 0) ud = 0.0;
-    S.t1[p] = M.A12[p] * ue;
-    S.t2[p] = M.A12[p] * ud;
+// kRaw: residual() feeds the raw derivatives to Laplace_operator instead (:437, no rules).
+template <bool kRaw = false>
+__device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh& M, CPlane u,
+                            Plane t1, Plane t2) {
+  const int nx = P.nx, ny = P.ny;
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
+    constexpr bool kIn = decltype(kin)::value;
+    double ud = dx1<kIn>(C, u, i, j, nx), ue = dy1<kIn>(C, u, i, j, ny);
+    if (!kRaw) {
+      if (j == 0 || j == nx - 1) ud = 0.0;
+      if (i == ny - 1) ue = 0.0;
+      if (i == 0) ud = 0.0;
+    }
+    t1(i, j) = M.A12[p] * ue;
+    t2(i, j) = M.A12[p] * ud;
   });
 }
 
-// The shared tail of the residual / pde_rhs chains, given u (point values) in `u`:
+// The shared tail of the residual / pde_rhs chains, given u (point values):
 //   stage L: v_xx, v_yy (explicit + cross terms t1 = A12 u_eta, t2 = A12 u_xi) -> u_xx, u_yy, p
 //   stage P: p derivatives with dp/dn = 0 -> p_x, p_y -> A, B
 //   stage F: F2 = J^-1 [d2eta A_xi - dksideta A_eta - dksideta B_xi + d2ksi B_eta]
-// The caller has filled S.ud / S.ue (u derivatives with its own boundary rules), S.t1, S.t2.
-// `u`, `a11`, `a22` share the row stride `ld`.  With `mon` set (the PMA loop) the stage writes the
-// raw monitor |u_xx + u_yy|^2 (:737) there instead of the pressure.
+// Stage L writes the pressure to `pout`, or with `mon` set (the PMA loop) the raw monitor
+// |u_xx + u_yy|^2 (:737) instead; u_xx / u_yy go to the optional point arrays uxx / uyy.
 __device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                                   const DropScratch& S, const double* u, const double* a11,
-                                   const double* a22, int ld, double* uxx, double* uyy,
-                                   double* mon = nullptr) {
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_, i = i_, j = j_;
-    const double vxx = lap_axis<kIn>(u + i * ld, a11 + i * ld, j, nx, 1, P.dksi * P.dksi);
-    const double vyy = lap_axis<kIn>(u + j, a22 + j, i, ny, ld, P.deta * P.deta);
-    double tx = dx1<kIn>(C, S.t1, i, j, nx, nx);
+                                   CPlane u, CPlane a11, CPlane a22, CPlane t1, CPlane t2,
+                                   double* uxx, double* uyy, double* mon, Plane pout) {
+  const int nx = P.nx, ny = P.ny;
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
+    constexpr bool kIn = decltype(kin)::value;
+    const double vxx = lap_axis<kIn>(u.v + i * u.ld, 1, a11.v + i * a11.ld, 1, j, nx,
+                                     P.dksi * P.dksi);
+    const double vyy = lap_axis<kIn>(u.v + j, u.ld, a22.v + j, a22.ld, i, ny, P.deta * P.deta);
+    double tx = dx1<kIn>(C, t1, i, j, nx);
     if (j == 0 || j == nx - 1) tx = 0.0;
-    double ty = dy1<kIn>(C, S.t2, i, j, ny, nx);
+    double ty = dy1<kIn>(C, t2, i, j, ny);
     if (i == 0 || i == ny - 1) ty = 0.0;
     const double hxx = (vxx + tx) / M.J[p];
     const double hyy = (vyy + ty) / M.J[p];
@@ -301,34 +325,33 @@ __device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const Dr
       const double s = fabs(hxx + hyy);
       mon[p] = s * s;
     } else {
-      S.p[p] = pressure(P, u[i * ld + j], hxx, hyy);
+      pout(i, j) = pressure(P, u(i, j), hxx, hyy);
     }
   });
 }
 
-__device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                              const DropScratch& S, const double* u) {
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_, i = i_, j = j_;
-    double pd = dx1<kIn>(C, S.p, i, j, nx, nx), pe = dy1<kIn>(C, S.p, i, j, ny, nx);
+// compute_P_spatial_ders (:683-694) and the pde_rhs fluxes A, B (:452-457)
+__device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMesh& M, CPlane pr,
+                              CPlane u, Plane A, Plane B) {
+  const int nx = P.nx, ny = P.ny;
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
+    constexpr bool kIn = decltype(kin)::value;
+    double pd = dx1<kIn>(C, pr, i, j, nx), pe = dy1<kIn>(C, pr, i, j, ny);
     if (j == 0 || j == nx - 1) pd = 0.0;
     if (i == 0 || i == ny - 1) pe = 0.0;
     const double pdx = (M.d2eta[p] * pd - M.dksideta[p] * pe) / M.J[p];
     const double pdy = (-M.dksideta[p] * pd + M.d2ksi[p] * pe) / M.J[p];
-    const double h3 = pow(u[p], 3.0);
-    S.A[p] = (pdx - P.Bo * sin(P.alpha2) / P.epsilon2) * h3 / 3;
-    S.B[p] = pdy * h3 / 3;
+    const double h3 = pow(u(i, j), 3.0);
+    A(i, j) = (pdx - P.Bo * sin(P.alpha2) / P.epsilon2) * h3 / 3;
+    B(i, j) = pdy * h3 / 3;
   });
 }
 
 template <bool kIn>
-__device__ __forceinline__ double flux_div_point(const Coefs& C, const DropMesh& M,
-                                                 const DropScratch& S, int p, int i, int j,
-                                                 int nx, int ny) {
-  return (M.d2eta[p] * dx1<kIn>(C, S.A, i, j, nx, nx) - M.dksideta[p] * dy1<kIn>(C, S.A, i, j, ny, nx)
-          - M.dksideta[p] * dx1<kIn>(C, S.B, i, j, nx, nx) + M.d2ksi[p] * dy1<kIn>(C, S.B, i, j, ny, nx)) /
+__device__ __forceinline__ double flux_div_point(const Coefs& C, const DropMesh& M, CPlane A,
+                                                 CPlane B, int p, int i, int j, int nx, int ny) {
+  return (M.d2eta[p] * dx1<kIn>(C, A, i, j, nx) - M.dksideta[p] * dy1<kIn>(C, A, i, j, ny)
+          - M.dksideta[p] * dx1<kIn>(C, B, i, j, nx) + M.d2ksi[p] * dy1<kIn>(C, B, i, j, ny)) /
          M.J[p];
 }
 
@@ -337,17 +360,26 @@ __global__ void __launch_bounds__(DB) drop_rhs_kernel(DropParams P, Coefs Ck, Dr
                                                       double* uxx, double* uyy, double* F) {
   const Coefs& C = Ck;
   coef_rows_init(C);
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  uders_stage(P, C, M, S, u, nx);
+  const int nx = P.nx, ny = P.ny;
+  const Plane t1{S.t1, nx}, t2{S.t2, nx}, pr{S.p, nx}, A{S.A, nx}, B{S.B, nx};
+  const CPlane uu(u, nx);
+  uders_stage(P, C, M, uu, t1, t2);
   __syncthreads();
-  lap_pressure_stage(P, C, M, S, u, M.A11, M.A22, nx, uxx, uyy);  // P.val = pressure(U.val, U.xx, U.yy) (:378)
+  // P.val = pressure(U.val, U.xx, U.yy) (:378)
+  lap_pressure_stage(P, C, M, uu, CPlane(M.A11, nx), CPlane(M.A22, nx), t1, t2, uxx, uyy,
+                     nullptr, pr);
   __syncthreads();
-  flux_AB_stage(P, C, M, S, u);  // compute_P_spatial_ders (:683-694), pde_rhs A, B (:456-457)
+  flux_AB_stage(P, C, M, pr, uu, A, B);
   __syncthreads();
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; F[p_] = flux_div_point<kIn>(C, M, S, p_, i_, j_, nx, ny); });
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
+    F[p] = flux_div_point<decltype(kin)::value>(C, M, A, B, p, i, j, nx, ny);
+  });
 }
 
+// residual(U, F, dt) (:435-450) and its forward-difference JVP, one launch per evaluation.
+// kLds: w stays in LDS plane L0 for the whole chain and every neighbour-read input (t1/t2, p,
+// A/B) is staged in planes L1/L2; otherwise all intermediates live in global scratch.
+template <bool kLds>
 __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, DropMesh M,
                                                         DropScratch S, const double* x,
                                                         const double* y, double alpha,
@@ -357,33 +389,41 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, 
                                                         double* partial) {
   const Coefs& C = Ck;
   coef_rows_init(C);
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    double w = x[p_];
-    if (y) w = w + alpha * y[p_];
-    S.w[p_] = w;
+  const int nx = P.nx, ny = P.ny, ld = kLds ? (nx | 1) : nx;
+  extern __shared__ double lds[];
+  const Plane W = kLds ? Plane{lds, ld} : Plane{S.w, nx};
+  const Plane L1 = kLds ? Plane{lds + ny * ld, ld} : Plane{S.t1, nx};
+  const Plane L2 = kLds ? Plane{lds + 2 * ny * ld, ld} : Plane{S.t2, nx};
+  const Plane gp{S.p, nx}, gB{S.B, nx};
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto) {
+    double w = x[p];
+    if (y) w = w + alpha * y[p];
+    W(i, j) = w;
   });
   __syncthreads();
-  // residual() feeds the raw derivatives to Laplace_operator (:437, no boundary rules)
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_, i = i_, j = j_;
-    const double ud = dx1<kIn>(C, S.w, i, j, nx, nx), ue = dy1<kIn>(C, S.w, i, j, ny, nx);
-    S.t1[p] = M.A12[p] * ue;
-    S.t2[p] = M.A12[p] * ud;
-  });
+  uders_stage<true>(P, C, M, W, L1, L2);  // t1 -> L1, t2 -> L2
   __syncthreads();
-  lap_pressure_stage(P, C, M, S, S.w, M.A11, M.A22, nx, nullptr, nullptr);
+  lap_pressure_stage(P, C, M, W, CPlane(M.A11, nx), CPlane(M.A22, nx), L1, L2, nullptr, nullptr,
+                     nullptr, gp);
   __syncthreads();
-  flux_AB_stage(P, C, M, S, S.w);
+  Plane pr = gp, A = {S.A, nx}, B = gB;
+  if (kLds) {  // p -> L1
+    for_points(nx, ny, [&](const int p, const int i, const int j, auto) { L1(i, j) = gp.v[p]; });
+    __syncthreads();
+    pr = L1;
+    A = L2;
+  }
+  flux_AB_stage(P, C, M, pr, W, A, B);
   __syncthreads();
+  if (kLds) {  // B -> L1 (p is dead)
+    for_points(nx, ny, [&](const int p, const int i, const int j, auto) { L1(i, j) = gB.v[p]; });
+    __syncthreads();
+    B = L1;
+  }
   double red[3] = {0.0, 0.0, 0.0};
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_;
-    const double F2 = flux_div_point<kIn>(C, M, S, p, i_, j_, nx, ny);
-    const double w = S.w[p];
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
+    const double F2 = flux_div_point<decltype(kin)::value>(C, M, A, B, p, i, j, nx, ny);
+    const double w = W(i, j);
     const double R = (w - uval[p]) - dt * (F2 + F[p]) / 2;  // (:450)
     if (mode == 0) {
       out[p] = R;
@@ -473,9 +513,10 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
       // compute_Q_spatial_ders, J, compute_u_spatial_ders (:595-597)
       mesh_stage(P, C, q, nx, M);
       __syncthreads();
-      uders_stage(P, C, M, S, uval, nx);
+      uders_stage(P, C, M, CPlane(uval, nx), Plane{S.t1, nx}, Plane{S.t2, nx});
       __syncthreads();
-      lap_pressure_stage(P, C, M, S, uval, M.A11, M.A22, nx, uxx, uyy, S.ud);
+      lap_pressure_stage(P, C, M, CPlane(uval, nx), CPlane(M.A11, nx), CPlane(M.A22, nx),
+                         CPlane(S.t1, nx), CPlane(S.t2, nx), uxx, uyy, S.ud, Plane{S.p, nx});
     } else {
       FOR_POINTS(NN) {
     [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
@@ -643,9 +684,10 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
       FOR_POINTS(NN) {
     [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = uval[p_]; });
       __syncthreads();
-      uders_stage(P, C, M, S, L0, ld);
+      uders_stage(P, C, M, CPlane(L0, ld), Plane{S.t1, nx}, Plane{S.t2, nx});
       __syncthreads();
-      lap_pressure_stage(P, C, M, S, L0, L1, L2, ld, S.A, S.B, S.ud);
+      lap_pressure_stage(P, C, M, CPlane(L0, ld), CPlane(L1, ld), CPlane(L2, ld),
+                         CPlane(S.t1, nx), CPlane(S.t2, nx), S.A, S.B, S.ud, Plane{S.p, nx});
       __syncthreads();
       FOR_POINTS(NN) {
     [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = S.ud[p_]; });
@@ -737,8 +779,19 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s) {
   if (!shape_ok(P)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(drop_resid_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, x, y,
-                     alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
+  const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
+  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
+  if (!force_global && lds <= kPmaLdsMax) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&drop_resid_kernel<true>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(drop_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S,
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
+  } else {
+    hipLaunchKernelGGL(drop_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S,
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
+  }
   return hipGetLastError();
 }
 
@@ -827,7 +880,7 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
     return t;
   }();
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
-  static const bool force_global = env_flag("NKHIP_PMA_GLOBAL") != 0;
+  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
   if (!force_global && lds <= kPmaLdsMax) {
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&drop_pma_lds_kernel),
