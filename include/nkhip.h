@@ -186,6 +186,38 @@ int nk_drop_residual(nk_drop* d, const double* u_dev, double dt, double* R_dev);
 int nk_drop_solve(nk_drop* d, double dt, double* U_dev, nk_stats* stats);         /* :383 */
 int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops);                       /* :589-599 */
 
+/* ---------------- MEMS on a moving mesh (python_work/PMA2_nk.py) ------------ */
+/* u_t = -(-Lap)^2 u - lambda/(1+u)^2 + lambda eps^(m-2)/(1+u)^m on [endl, endr]^2 (N x N), one
+ * PMA mesh step per time step.  Parameters = the module globals of PMA2_nk.py:22-37.  Only p = 2
+ * exists: the reference's p = 1 branch of residual() raises (u.xx, :135). */
+typedef struct nk_mems_params {
+  int32_t n;                    /* 51 (:22) */
+  int32_t m;                    /* 3 (:25) */
+  int32_t smoothing_iters;      /* 4 (:30) */
+  int32_t p;                    /* 2 (:24); anything else is NK_EINVAL */
+  double alpha, gamma;          /* PMA: 0.1, 0.1 (:26-27) */
+  double epsilon, beta, lambd;  /* 0, 0.15, 1 (:28-29, :31) */
+  double endl, endr;            /* -1, 1 (:32) */
+  double k;                     /* 1e-4 (:36): the dt residual() divides by (quirk, :51/:91) */
+} nk_mems_params;
+typedef struct nk_mems nk_mems;
+
+int nk_mems_params_default(nk_mems_params* p);
+int nk_mems_create(nk_mems** out, const nk_mems_params* p, const nk_opts* opts, void* stream);
+int nk_mems_destroy(nk_mems* m);
+/* state: U.new (= U.val) and Q.val, device arrays of n*n */
+int nk_mems_set_state(nk_mems* m, const double* U_dev, const double* Q_dev);
+int nk_mems_get_state(nk_mems* m, double* U_dev, double* Q_dev);
+/* one pass of main()'s loop (PMA2_nk.py:77-103): U.val = U.new; mesh fields; dt = compute_g()*k;
+ * solve_PMA; CN_term; U.new = newton_krylov(residual, U.val) with the nk_opts given at creation
+ * (the reference: SciPy defaults, :97); Q.val += dt*Q.dt.  *dt_used = dt, *time = the clock. */
+int nk_mems_step(nk_mems* m, nk_stats* stats, double* dt_used, double* time);
+/* pieces (tests / tooling): prepare = :80-94 for the current state, *dt = compute_g()*k */
+int nk_mems_prepare(nk_mems* m, double* dt);
+/* which: as nk_drop_field, with 9 = CN_term */
+int nk_mems_field(nk_mems* m, int32_t which, double* out_dev);
+int nk_mems_residual(nk_mems* m, const double* u_dev, double* R_dev); /* :121-159 */
+
 #ifdef __cplusplus
 }
 #endif

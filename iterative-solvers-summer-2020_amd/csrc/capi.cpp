@@ -12,6 +12,7 @@
 #include "nk_kernels.h"
 #include "nk_solver.h"
 #include "droplet_problem.h"
+#include "mems_problem.h"
 #include "sh_problem.h"
 
 using namespace nk;
@@ -420,6 +421,83 @@ int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops) {
   if (!d || loops < 1) return NK_EINVAL;
   const int rc = DS(d)->pma(dtmesh, loops);
   return rc ? rc : DS(d)->E.sync();
+}
+
+// ------------------------------------------------------------------------------ PMA2 (MEMS)
+int nk_mems_params_default(nk_mems_params* p) {
+  if (!p) return NK_EINVAL;
+  *p = nk_mems_params{};
+  p->n = 51;
+  p->m = 3;
+  p->smoothing_iters = 4;
+  p->p = 2;
+  p->alpha = 0.1;
+  p->gamma = 0.1;
+  p->epsilon = 0.0;
+  p->beta = 0.15;
+  p->lambd = 1.0;
+  p->endl = -1.0;
+  p->endr = 1.0;
+  p->k = 1e-4;
+  return NK_OK;
+}
+
+int nk_mems_create(nk_mems** out, const nk_mems_params* p, const nk_opts* opts, void* stream) {
+  if (!out || !p || p->n < 7 || p->p != 2 || p->m < 0 || !(p->endr > p->endl)) return NK_EINVAL;
+  DropParams P{};
+  P.nx = P.ny = p->n;
+  P.endl = P.endb = p->endl;
+  P.endr = P.endt = p->endr;
+  P.dksi = P.deta = (p->endr - p->endl) / (p->n - 1);  // PMA2_nk.py:33-34
+  P.alpha = p->alpha;
+  P.gamma = p->gamma;
+  P.C = 1.0;  // mon += integral (:384)
+  P.smoothing_iters = p->smoothing_iters;
+  MemsParams Mp{};
+  Mp.lambd = p->lambd;
+  Mp.lam_eps = p->lambd * std::pow(p->epsilon, double(p->m - 2));  // lambd_*(epsilon_**(m_-2))
+  Mp.beta2 = p->beta * p->beta;
+  Mp.k = p->k;
+  Mp.m = p->m;
+  const nk_opts o = opts ? *opts : default_opts();
+  std::unique_ptr<MemsStepper> m(new (std::nothrow) MemsStepper(P, Mp, p->epsilon, o, S(stream)));
+  if (!m) return NK_ENOMEM;
+  if (m->status()) return m->status();
+  *out = reinterpret_cast<nk_mems*>(m.release());
+  return NK_OK;
+}
+
+static MemsStepper* MS(nk_mems* m) { return reinterpret_cast<MemsStepper*>(m); }
+
+int nk_mems_destroy(nk_mems* m) {
+  delete MS(m);
+  return NK_OK;
+}
+int nk_mems_set_state(nk_mems* m, const double* U, const double* Q) {
+  if (!m || !U || !Q) return NK_EINVAL;
+  MS(m)->time = 0.0;
+  return MS(m)->set_state(U, Q);
+}
+int nk_mems_get_state(nk_mems* m, double* U, double* Q) {
+  return m ? MS(m)->get_state(U, Q) : NK_EINVAL;
+}
+int nk_mems_step(nk_mems* m, nk_stats* stats, double* dt_used, double* time) {
+  if (!m) return NK_EINVAL;
+  const int rc = MS(m)->step(stats, dt_used);
+  if (time) *time = MS(m)->time;
+  return rc;
+}
+int nk_mems_prepare(nk_mems* m, double* dt) {
+  if (!m) return NK_EINVAL;
+  int rc = MS(m)->E.copy(MS(m)->P.uval, MS(m)->P.unew, MS(m)->E.n);
+  if (!rc) rc = MS(m)->prepare(dt);
+  return rc ? rc : MS(m)->E.sync();
+}
+int nk_mems_field(nk_mems* m, int32_t which, double* out) {
+  return (m && out) ? MS(m)->field(which, out) : NK_EINVAL;
+}
+int nk_mems_residual(nk_mems* m, const double* u, double* R) {
+  return (m && u && R) ? MS(m)->residual(u, R) : NK_EINVAL;
 }
 
 }  // extern "C"

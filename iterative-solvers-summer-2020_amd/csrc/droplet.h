@@ -56,6 +56,27 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s);
 
+// PMA2 (python_work/PMA2_nk.py) physics on the same mapped mesh (:121-159, :400-413):
+//   new_rhs(u) = -lambda/(1+u)^2 + lambda eps^(m-2)/(1+u)^m - beta^2 Lap(Lap u), 0 on the boundary
+//   residual(u) = (u - U.val)/k - (new_rhs(u) + CN_term)/2
+struct MemsParams {
+  double lambd;    // lambda (:30)
+  double lam_eps;  // lambda * eps^(m-2), evaluated on the host as the reference does
+  double beta2;    // beta*beta
+  double k;        // the global dt = k used by residual() (:51)
+  int m;
+  int pad_;
+};
+
+// mode 0: out = residual(x + alpha y), xt = x + alpha y, partial[0..2] = (sum R^2, max|R|, max|x|)
+// mode 1: out = (residual(x + alpha y) - f0)/sc                          (forward-difference JVP)
+// mode 2: out = new_rhs(x) (CN_term), uxx/uyy = Laplace_operator(x) (compute_u_spatial_ders),
+//         partial[0] = max(-(1+x)^3), i.e. -compute_g() (:437-441)
+hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh M, DropScratch S,
+                             const double* x, const double* y, double alpha, const double* uval,
+                             const double* cn, int mode, const double* f0, double sc, double* out,
+                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s);
+
 // Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
 // Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the four DCT operands of the MFMA path in
 // v_mfma_f64_16x16x4 fragment order (zero-padded to 16-row/column tiles and 4-deep k steps):
@@ -72,9 +93,12 @@ PmaTables drop_pma_view(const DropParams& P, const double* packed);
 
 // The PMA mesh loop loop_pma(dtm, loops) (:589-599) in one persistent single-workgroup launch.
 // The first iteration uses the caller's u_xx, u_yy (and the mesh fields in M); q is updated in
-// place.
+// place.  Monitor (compute_and_smooth_monitor): kMonLap = |u_xx + u_yy|^2 (droplet.py:737,
+// PMA2_nk.py:361 for eps > 0, p = 2); kMonGap = 1/(1+u)^6 from uval (PMA2_nk.py:357, eps = 0).
+enum { kMonLap = 0, kMonGap = 1 };
 hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, double* q,
                            const double* uval, const double* uxx0, const double* uyy0,
-                           const PmaTables& T, double dtm, int loops, hipStream_t s);
+                           const PmaTables& T, double dtm, int loops, hipStream_t s,
+                           int monitor = kMonLap);
 
 }  // namespace nk

@@ -298,15 +298,12 @@ __device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh&
   });
 }
 
-// The shared tail of the residual / pde_rhs chains, given u (point values):
-//   stage L: v_xx, v_yy (explicit + cross terms t1 = A12 u_eta, t2 = A12 u_xi) -> u_xx, u_yy, p
-//   stage P: p derivatives with dp/dn = 0 -> p_x, p_y -> A, B
-//   stage F: F2 = J^-1 [d2eta A_xi - dksideta A_eta - dksideta B_xi + d2ksi B_eta]
-// Stage L writes the pressure to `pout`, or with `mon` set (the PMA loop) the raw monitor
-// |u_xx + u_yy|^2 (:737) instead; u_xx / u_yy go to the optional point arrays uxx / uyy.
-__device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
-                                   CPlane u, CPlane a11, CPlane a22, CPlane t1, CPlane t2,
-                                   double* uxx, double* uyy, double* mon, Plane pout) {
+// Laplace_operator (:601-681) at every point: f(p, i, j, u_xx, u_yy) with
+//   u_xx = J^-1 [(A11 u_xi)_xi explicit stencil + (A12 u_eta)_xi], u_yy likewise,
+// given the cross-term inputs t1 = A12 u_eta, t2 = A12 u_xi.
+template <class F>
+__device__ void lap_stage(const DropParams& P, const Coefs& C, const DropMesh& M, CPlane u,
+                          CPlane a11, CPlane a22, CPlane t1, CPlane t2, F f) {
   const int nx = P.nx, ny = P.ny;
   for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
     constexpr bool kIn = decltype(kin)::value;
@@ -317,17 +314,30 @@ __device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const Dr
     if (j == 0 || j == nx - 1) tx = 0.0;
     double ty = dy1<kIn>(C, t2, i, j, ny);
     if (i == 0 || i == ny - 1) ty = 0.0;
-    const double hxx = (vxx + tx) / M.J[p];
-    const double hyy = (vyy + ty) / M.J[p];
-    if (uxx) uxx[p] = hxx;
-    if (uyy) uyy[p] = hyy;
-    if (mon) {
-      const double s = fabs(hxx + hyy);
-      mon[p] = s * s;
-    } else {
-      pout(i, j) = pressure(P, u(i, j), hxx, hyy);
-    }
+    f(p, i, j, (vxx + tx) / M.J[p], (vyy + ty) / M.J[p]);
   });
+}
+
+// The shared tail of the residual / pde_rhs chains, given u (point values):
+//   stage L: v_xx, v_yy (explicit + cross terms t1 = A12 u_eta, t2 = A12 u_xi) -> u_xx, u_yy, p
+//   stage P: p derivatives with dp/dn = 0 -> p_x, p_y -> A, B
+//   stage F: F2 = J^-1 [d2eta A_xi - dksideta A_eta - dksideta B_xi + d2ksi B_eta]
+// Stage L writes the pressure to `pout`, or with `mon` set (the PMA loop) the raw monitor
+// |u_xx + u_yy|^2 (:737) instead; u_xx / u_yy go to the optional point arrays uxx / uyy.
+__device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const DropMesh& M,
+                                   CPlane u, CPlane a11, CPlane a22, CPlane t1, CPlane t2,
+                                   double* uxx, double* uyy, double* mon, Plane pout) {
+  lap_stage(P, C, M, u, a11, a22, t1, t2,
+            [&](const int p, const int i, const int j, const double hxx, const double hyy) {
+              if (uxx) uxx[p] = hxx;
+              if (uyy) uyy[p] = hyy;
+              if (mon) {
+                const double s = fabs(hxx + hyy);
+                mon[p] = s * s;
+              } else {
+                pout(i, j) = pressure(P, u(i, j), hxx, hyy);
+              }
+            });
 }
 
 // compute_P_spatial_ders (:683-694) and the pde_rhs fluxes A, B (:452-457)
@@ -441,6 +451,86 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, 
   }
 }
 
+// ---------------------------------------------------------------------------- PMA2 (MEMS)
+// PMA2_nk.py residual() (:121-159) / compute_rhs_pde() (:400-413): the bilaplacian chain
+//   u -> (u_xx, u_yy) = Laplace_operator(u) -> v = u_xx + u_yy -> (v_xx, v_yy) = Laplace_operator(v)
+// with raw centred derivatives feeding each Laplace_operator (:133, :141).  kLds: w, v and the
+// cross-term inputs live in three LDS planes; otherwise in global scratch.
+template <bool kLds>
+__global__ void __launch_bounds__(DB) mems_resid_kernel(DropParams P, Coefs Ck, MemsParams Mp,
+                                                        DropMesh M, DropScratch S, const double* x,
+                                                        const double* y, double alpha,
+                                                        const double* uval, const double* cn,
+                                                        int mode, const double* f0, double sc,
+                                                        double* out, double* xt, double* uxx,
+                                                        double* uyy, double* partial) {
+  const Coefs& C = Ck;
+  coef_rows_init(C);
+  const int nx = P.nx, ny = P.ny, ld = kLds ? (nx | 1) : nx;
+  extern __shared__ double lds[];
+  const Plane W = kLds ? Plane{lds, ld} : Plane{S.w, nx};
+  const Plane L1 = kLds ? Plane{lds + ny * ld, ld} : Plane{S.t1, nx};
+  const Plane L2 = kLds ? Plane{lds + 2 * ny * ld, ld} : Plane{S.t2, nx};
+  const Plane V = kLds ? W : Plane{S.p, nx};  // v = u_xx + u_yy (LDS: reuses w's plane)
+  const CPlane A11(M.A11, nx), A22(M.A22, nx);
+  for_points(nx, ny, [&](const int p, const int i, const int j, auto) {
+    double w = x[p];
+    if (y) w = w + alpha * y[p];
+    W(i, j) = w;
+    if (kLds) S.w[p] = w;  // read back point-wise once W's plane holds v
+  });
+  __syncthreads();
+  uders_stage<true>(P, C, M, W, L1, L2);
+  __syncthreads();
+  lap_stage(P, C, M, W, A11, A22, L1, L2,
+            [&](const int p, const int, const int, const double hxx, const double hyy) {
+              if (mode == 2 && uxx) {
+                uxx[p] = hxx;
+                uyy[p] = hyy;
+              }
+              S.p[p] = hxx + hyy;
+            });
+  __syncthreads();
+  if (kLds) {
+    for_points(nx, ny, [&](const int p, const int i, const int j, auto) { V(i, j) = S.p[p]; });
+    __syncthreads();
+  }
+  uders_stage<true>(P, C, M, V, L1, L2);
+  __syncthreads();
+  double red[3] = {0.0, 0.0, 0.0};
+  if (mode == 2) red[0] = -INFINITY;
+  lap_stage(P, C, M, V, A11, A22, L1, L2,
+            [&](const int p, const int i, const int j, const double vxx, const double vyy) {
+              const double w = S.w[p];
+              const double g = 1 + w;
+              double r = -Mp.lambd / (g * g) + Mp.lam_eps / pow(g, double(Mp.m));
+              r = r - Mp.beta2 * (vxx + vyy);
+              if (i == 0 || j == 0 || i == ny - 1 || j == nx - 1) r = 0.0;  // (:157)
+              if (mode == 2) {
+                out[p] = r;
+                red[0] = nmax(red[0], -pow(g, 3.0));
+                return;
+              }
+              const double R = (w - uval[p]) / Mp.k - (r + cn[p]) / 2;  // (:159)
+              if (mode == 0) {
+                out[p] = R;
+                if (xt) xt[p] = w;
+                red[0] += R * R;
+                red[1] = nmax(red[1], fabs(R));
+                red[2] = nmax(red[2], fabs(w));
+              } else {
+                out[p] = (R - f0[p]) / sc;
+              }
+            });
+  if (mode == 0) {
+    const double v = block_reduce<3, 1, DB>(red);
+    if (threadIdx.x < 3) partial[threadIdx.x] = v;
+  } else if (mode == 2) {
+    const double v = block_reduce<3, 0, DB>(red);  // all-max; only red[0] is meaningful
+    if (threadIdx.x == 0) partial[0] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------- PMA mesh loop
 // loop_pma (:589-599), solve_PMA (:578-587), compute_and_smooth_monitor (:729-760) as ONE
 // persistent single-workgroup kernel running all `loops` iterations on the GPU.  The orthonormal
@@ -489,8 +579,7 @@ __device__ double monitor_integral(const DropParams& P, const DropMesh& M, const
                                    double* bcast) {
   const int nx = P.nx, ny = P.ny;
   double part[1] = {0.0};
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; part[0] += T[i_ * ld + j_] * fabs(M.J[p_]); });
+  FOR_POINTS(NN) { part[0] += T[i_ * ld + j_] * fabs(M.J[p_]); });
   const double tot = block_reduce<1, 1, DB>(part);
   if (threadIdx.x == 0) *bcast = tot * P.dksi * P.deta;
   __syncthreads();
@@ -501,7 +590,8 @@ __device__ double monitor_integral(const DropParams& P, const DropMesh& M, const
 __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, DropMesh M,
                                                       DropScratch S, double* q, const double* uval,
                                                       const double* uxx0, const double* uyy0,
-                                                      PmaTables Tb, double dtm, int loops) {
+                                                      PmaTables Tb, double dtm, int loops,
+                                                      int monitor) {
   const Coefs& C = Ck;
   coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
@@ -509,7 +599,12 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
   double* uxx = S.A;  // u_xx, u_yy of the current mesh (first iteration: the caller's)
   double* uyy = S.B;
   for (int it = 0; it < loops; ++it) {
-    if (it > 0) {
+    if (monitor == kMonGap) {
+      FOR_POINTS(NN) { S.ud[p_] = 1 / pow(1 + uval[p_], 6.0); });  // (PMA2_nk.py:357)
+      if (it > 0) {
+        mesh_stage(P, C, q, nx, M);
+      }
+    } else if (it > 0) {
       // compute_Q_spatial_ders, J, compute_u_spatial_ders (:595-597)
       mesh_stage(P, C, q, nx, M);
       __syncthreads();
@@ -519,7 +614,6 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
                          CPlane(S.t1, nx), CPlane(S.t2, nx), uxx, uyy, S.ud, Plane{S.p, nx});
     } else {
       FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
         const double s = fabs(uxx0[p_] + uyy0[p_]);  // monitor |u_xx + u_yy|^2 (:737)
         S.ud[p_] = s * s;
       });
@@ -537,8 +631,7 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
     const double integral = monitor_integral(P, M, T, nx, &bcast);
     // q_rhs = sqrt(mon |J|) / alpha (:584)
     double* X = S.p;
-    FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; X[p_] = sqrt((T[p_] + P.C * integral) * fabs(M.J[p_])) / P.alpha; });
+    FOR_POINTS(NN) { X[p_] = sqrt((T[p_] + P.C * integral) * fabs(M.J[p_])) / P.alpha; });
     __syncthreads();
     // 2-D DCT-II ortho: T1 = Cy X (along eta), T2 = T1 Cx^T (along xi) (:585)
     double* T1 = S.t1;
@@ -652,7 +745,8 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
     DropParams P, Coefs Ck, DropMesh M, DropScratch S, double* q, const double* uval,
     const double* uxx0, const double* uyy0, const double* __restrict__ fa1,
     const double* __restrict__ fb2, const double* __restrict__ fa3, const double* __restrict__ fb4,
-    const double* __restrict__ den, double dtm, int loops, unsigned long long* tprof) {
+    const double* __restrict__ den, double dtm, int loops, int monitor,
+    unsigned long long* tprof) {
   const Coefs& C = Ck;
   coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny, ld = nx | 1;
@@ -672,29 +766,33 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
   };
   mark(-1);
   for (int it = 0; it < loops; ++it) {
-    if (it > 0) {
+    if (monitor == kMonGap) {
+      if (it > 0) {  // the mesh fields (J) of the updated q
+        FOR_POINTS(NN) { L0[i_ * ld + j_] = q[p_]; });
+        __syncthreads();
+        mesh_stage(P, C, L0, ld, M);
+        __syncthreads();
+      }
+      FOR_POINTS(NN) { L0[i_ * ld + j_] = 1 / pow(1 + uval[p_], 6.0); });  // (PMA2_nk.py:357)
+    } else if (it > 0) {
       // compute_Q_spatial_ders + J (:595-596) from q staged in L0; A11 -> L1, A22 -> L2
-      FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = q[p_]; });
+      FOR_POINTS(NN) { L0[i_ * ld + j_] = q[p_]; });
       __syncthreads();
       mesh_stage(P, C, L0, ld, M, L1, L2);
       __syncthreads();
       mark(0);
       // compute_u_spatial_ders (:597) from u staged in L0
-      FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = uval[p_]; });
+      FOR_POINTS(NN) { L0[i_ * ld + j_] = uval[p_]; });
       __syncthreads();
       uders_stage(P, C, M, CPlane(L0, ld), Plane{S.t1, nx}, Plane{S.t2, nx});
       __syncthreads();
       lap_pressure_stage(P, C, M, CPlane(L0, ld), CPlane(L1, ld), CPlane(L2, ld),
                          CPlane(S.t1, nx), CPlane(S.t2, nx), S.A, S.B, S.ud, Plane{S.p, nx});
       __syncthreads();
-      FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value; L0[i_ * ld + j_] = S.ud[p_]; });
+      FOR_POINTS(NN) { L0[i_ * ld + j_] = S.ud[p_]; });
       mark(1);
     } else {
       FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
         const double s = fabs(uxx0[p_] + uyy0[p_]);  // monitor |u_xx + u_yy|^2 (:737)
         L0[i_ * ld + j_] = s * s;
       });
@@ -795,6 +893,27 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
   return hipGetLastError();
 }
 
+hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh M, DropScratch S,
+                             const double* x, const double* y, double alpha, const double* uval,
+                             const double* cn, int mode, const double* f0, double sc, double* out,
+                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s) {
+  if (!shape_ok(P) || mode < 0 || mode > 2) return hipErrorInvalidValue;
+  const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
+  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
+  if (!force_global && lds <= kPmaLdsMax) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&mems_resid_kernel<true>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(mems_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), Mp,
+                       M, S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial);
+  } else {
+    hipLaunchKernelGGL(mems_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), Mp, M,
+                       S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial);
+  }
+  return hipGetLastError();
+}
+
 // Host side: DCT matrices, the (1 - gamma Leig) divisor and the MFMA fragment tables, uploaded
 // once per stepper.
 namespace {
@@ -872,8 +991,10 @@ std::vector<double> drop_pma_tables(const DropParams& P) {
 
 hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, double* q,
                            const double* uval, const double* uxx0, const double* uyy0,
-                           const PmaTables& T, double dtm, int loops, hipStream_t s) {
-  if (!shape_ok(P) || loops < 1) return hipErrorInvalidValue;
+                           const PmaTables& T, double dtm, int loops, hipStream_t s,
+                           int monitor) {
+  if (!shape_ok(P) || loops < 1 || (monitor != kMonLap && monitor != kMonGap))
+    return hipErrorInvalidValue;
   static unsigned long long* tprof = [] {
     unsigned long long* t = nullptr;
     if (env_flag("NKHIP_PMA_TIMING") && hipMalloc(&t, 64) != hipSuccess) t = nullptr;
@@ -887,10 +1008,11 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(drop_pma_lds_kernel, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S, q,
-                       uval, uxx0, uyy0, T.fa1, T.fb2, T.fa3, T.fb4, T.den, dtm, loops, tprof);
+                       uval, uxx0, uyy0, T.fa1, T.fb2, T.fa3, T.fb4, T.den, dtm, loops, monitor,
+                       tprof);
   } else {
     hipLaunchKernelGGL(drop_pma_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, q, uval,
-                       uxx0, uyy0, T, dtm, loops);
+                       uxx0, uyy0, T, dtm, loops, monitor);
   }
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && tprof && !force_global) {

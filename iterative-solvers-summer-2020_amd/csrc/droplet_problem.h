@@ -8,7 +8,7 @@
 
 namespace nk {
 
-class DropletProblem final : public Problem {
+class DropletProblem : public Problem {
  public:
   DropletProblem(Engine& E, const DropParams& P);
   ~DropletProblem() override;
@@ -24,12 +24,13 @@ class DropletProblem final : public Problem {
   const DropMesh& mesh() const { return M_; }
   const DropScratch& scratch() const { return S_; }
   const DropParams& params() const { return P_; }
+  double dt() const { return dt_; }
 
   // state and per-step fields (device, nx*ny each)
   double *uval = nullptr, *unew = nullptr, *qval = nullptr, *F = nullptr, *uxx = nullptr,
          *uyy = nullptr, *tmp = nullptr, *tmp2 = nullptr;
 
- private:
+ protected:
   Engine& E_;
   DropParams P_;
   DropMesh M_{};

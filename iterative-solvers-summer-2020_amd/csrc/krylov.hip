@@ -174,7 +174,8 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial
   const int k = blockIdx.x;
   const bool is_sum = k < nsum;
   const double* p = partial + int64_t(k) * nblk;
-  double acc = 0.0;
+  // max reductions start from -inf (signed quantities such as -min(...) are allowed)
+  double acc = is_sum ? 0.0 : -INFINITY;
   for (int64_t b = threadIdx.x; b < nblk; b += 256) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
   double v[1] = {acc};
   // the reduction tree is fixed, so the result does not depend on timing
@@ -184,6 +185,7 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial
   } else {
     s = block_reduce<1, 0, 256>(v);
   }
+  if (nblk == 0) s = 0.0;  // empty input
   if (threadIdx.x == 0) {
     result[k] = s;
     if (result_host) result_host[k] = s;  // pinned, device-mapped host memory: no D2H blit

@@ -52,6 +52,13 @@ class nk_drop_params(C.Structure):
                 ("C", C.c_double), ("smoothing_iters", C.c_int32), ("pad_", C.c_int32)]
 
 
+class nk_mems_params(C.Structure):
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("smoothing_iters", C.c_int32),
+                ("p", C.c_int32), ("alpha", C.c_double), ("gamma", C.c_double),
+                ("epsilon", C.c_double), ("beta", C.c_double), ("lambd", C.c_double),
+                ("endl", C.c_double), ("endr", C.c_double), ("k", C.c_double)]
+
+
 RESIDUAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
 
 _P = C.c_void_p
@@ -105,6 +112,16 @@ SIGNATURES = [
     ("nk_drop_residual", C.c_int, [_P, _P, _D, _P]),
     ("nk_drop_solve", C.c_int, [_P, _D, _P, C.POINTER(nk_stats)]),
     ("nk_drop_pma", C.c_int, [_P, _D, _I32]),
+    ("nk_mems_params_default", C.c_int, [C.POINTER(nk_mems_params)]),
+    ("nk_mems_create", C.c_int, [C.POINTER(_P), C.POINTER(nk_mems_params), C.POINTER(nk_opts),
+                                 _P]),
+    ("nk_mems_destroy", C.c_int, [_P]),
+    ("nk_mems_set_state", C.c_int, [_P, _P, _P]),
+    ("nk_mems_get_state", C.c_int, [_P, _P, _P]),
+    ("nk_mems_step", C.c_int, [_P, C.POINTER(nk_stats), C.POINTER(_D), C.POINTER(_D)]),
+    ("nk_mems_prepare", C.c_int, [_P, C.POINTER(_D)]),
+    ("nk_mems_field", C.c_int, [_P, _I32, _P]),
+    ("nk_mems_residual", C.c_int, [_P, _P, _P]),
 ]
 
 
