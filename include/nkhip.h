@@ -161,6 +161,7 @@ typedef struct nk_drop_params {
   double alpha, gamma, C;         /* PMA: 0.01, 0.1, 0.15 (:40-42) */
   int32_t smoothing_iters;        /* 4 (:31) */
   int32_t pad_;
+  double a;                       /* droplet profile sharpness 100 (:24) */
 } nk_drop_params;
 typedef struct nk_drop nk_drop;
 
@@ -185,6 +186,13 @@ int nk_drop_field(nk_drop* d, int32_t which, double* out_dev);
 int nk_drop_residual(nk_drop* d, const double* u_dev, double dt, double* R_dev); /* :435-450 */
 int nk_drop_solve(nk_drop* d, double dt, double* U_dev, nk_stats* stats);         /* :383 */
 int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops);                       /* :589-599 */
+/* initialise_coalescing_droplets (droplet.py:132-189) from the current state (normally U = epsilon,
+ * Q = (xi^2 + eta^2)/2, main() :103-106): `info` (host) holds ndrops <= 8 (x, y, R, V) rows; the
+ * volumes grow linearly over vsteps steps, each followed by loop_pma(dtmesh, loops).  The
+ * reference runs (1000, [[0,0,1,1],[3,0,1,1]], 5e-9, 20) and saves the result as
+ * initdrop_coal_*.txt. */
+int nk_drop_init_coalescing(nk_drop* d, int32_t vsteps, const double* info, int32_t ndrops,
+                            double dtmesh, int32_t loops);
 
 /* ---------------- MEMS on a moving mesh (python_work/PMA2_nk.py) ------------ */
 /* u_t = -(-Lap)^2 u - lambda/(1+u)^2 + lambda eps^(m-2)/(1+u)^m on [endl, endr]^2 (N x N), one

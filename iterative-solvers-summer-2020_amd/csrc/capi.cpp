@@ -346,6 +346,7 @@ int nk_drop_params_default(nk_drop_params* p) {
   p->gamma = 0.1;
   p->C = 0.15;
   p->smoothing_iters = 4;
+  p->a = 100.0;
   return NK_OK;
 }
 
@@ -370,6 +371,7 @@ int nk_drop_create(nk_drop** out, const nk_drop_params* p, const nk_opts* opts, 
   P.gamma = p->gamma;
   P.C = p->C;
   P.smoothing_iters = p->smoothing_iters;
+  P.a = p->a;
   const nk_opts o = opts ? *opts : default_opts();
   std::unique_ptr<DropletStepper> d(new (std::nothrow) DropletStepper(P, o, S(stream)));
   if (!d) return NK_ENOMEM;
@@ -421,6 +423,17 @@ int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops) {
   if (!d || loops < 1) return NK_EINVAL;
   const int rc = DS(d)->pma(dtmesh, loops);
   return rc ? rc : DS(d)->E.sync();
+}
+
+int nk_drop_init_coalescing(nk_drop* d, int32_t vsteps, const double* info, int32_t ndrops,
+                            double dtmesh, int32_t loops) {
+  if (!d || vsteps < 1 || loops < 0 || ndrops < 0 || ndrops > kMaxDrops || (ndrops && !info))
+    return NK_EINVAL;
+  DropSet D{};
+  D.n = ndrops;
+  for (int k = 0; k < ndrops; ++k)
+    for (int c = 0; c < 4; ++c) D.v[k][c] = info[4 * k + c];
+  return DS(d)->init_coalescing(vsteps, D, dtmesh, loops);
 }
 
 // ------------------------------------------------------------------------------ PMA2 (MEMS)

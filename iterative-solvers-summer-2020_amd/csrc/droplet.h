@@ -25,6 +25,7 @@ struct DropParams {
   double Bo, alpha2, epsilon2;    // Bond number, inclination, Ho/Lo (:47,50-51)
   double alpha, gamma, C;         // PMA: adaption speed, smoothing, Mackenzie constant (:40-42)
   int smoothing_iters;            // (:31)
+  double a;                       // droplet profile sharpness of G/G2 (:24)
 };
 
 // Per-time-step fields of the mesh potential Q (compute_Q_spatial_ders :696-711, J :376) and
@@ -55,6 +56,16 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              const double* y, double alpha, const double* uval, const double* F,
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s);
+
+// compute_U2 (:413-423): u = eps + sum_d (1-eps) H2(G2(|x - x_d|, R_d), R_d, V_d) at the node
+// coordinates x = (M.dksi, M.deta); `drops` holds ndrops (x, y, R, V) quadruples (by value).
+constexpr int kMaxDrops = 8;
+struct DropSet {
+  double v[kMaxDrops][4];
+  int n;
+};
+hipError_t drop_u2_launch(const DropParams& P, DropMesh M, const DropSet& drops, double* u,
+                          hipStream_t s);
 
 // PMA2 (python_work/PMA2_nk.py) physics on the same mapped mesh (:121-159, :400-413):
 //   new_rhs(u) = -lambda/(1+u)^2 + lambda eps^(m-2)/(1+u)^m - beta^2 Lap(Lap u), 0 on the boundary

@@ -451,6 +451,24 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, 
   }
 }
 
+// ---------------------------------------------------------------------------- droplet init
+// compute_U2 (:413-429) at the node coordinates of the current mesh.
+__global__ void __launch_bounds__(256) drop_u2_kernel(DropParams P, DropMesh M, DropSet D,
+                                                      double* u) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P.nx * P.ny) return;
+  const double xp = M.dksi[p], yp = M.deta[p];
+  double r = P.epsilon;
+  for (int d = 0; d < D.n; ++d) {
+    const double x = D.v[d][0], y = D.v[d][1], R = D.v[d][2], V = D.v[d][3];
+    const double xx = sqrt((xp - x) * (xp - x) + (yp - y) * (yp - y));
+    const double psi =
+        R + log((1 + exp(-2 * P.a * (xx + R))) / (1 + exp(-2 * P.a * (xx - R)))) / (2 * P.a);
+    r += (1 - P.epsilon) * (4 * V * (1 - psi * psi / (R * R)) / (R * R));
+  }
+  u[p] = r;
+}
+
 // ---------------------------------------------------------------------------- PMA2 (MEMS)
 // PMA2_nk.py residual() (:121-159) / compute_rhs_pde() (:400-413): the bilaplacian chain
 //   u -> (u_xx, u_yy) = Laplace_operator(u) -> v = u_xx + u_yy -> (v_xx, v_yy) = Laplace_operator(v)
@@ -890,6 +908,14 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
     hipLaunchKernelGGL(drop_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S,
                        x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
   }
+  return hipGetLastError();
+}
+
+hipError_t drop_u2_launch(const DropParams& P, DropMesh M, const DropSet& drops, double* u,
+                          hipStream_t s) {
+  if (!shape_ok(P) || drops.n < 0 || drops.n > kMaxDrops) return hipErrorInvalidValue;
+  const int n = P.nx * P.ny;
+  hipLaunchKernelGGL(drop_u2_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P, M, drops, u);
   return hipGetLastError();
 }
 

@@ -170,6 +170,22 @@ int DropletStepper::step(double dt, double dtm, int loops, nk_stats* st, double*
   return NK_OK;
 }
 
+int DropletStepper::init_coalescing(int vsteps, const DropSet& drops, double dtm, int loops) {
+  DropSet arg = drops;
+  for (int i = 1; i <= vsteps; ++i) {
+    int rc = E.copy(P.uval, P.unew, E.n);  // U.val = U.new.copy() (:158)
+    if (!rc) rc = prepare();                // mesh fields, J, U.xx/U.yy (:160-163)
+    for (int d = 0; d < drops.n; ++d) arg.v[d][3] = drops.v[d][3] * i / vsteps;  // :165-166
+    if (!rc) rc = E.launch(K_USERF, 0.0, [&] {
+      return drop_u2_launch(P.params(), P.mesh(), arg, P.unew, E.s);  // :167
+    });
+    if (!rc && loops > 0) rc = pma(dtm, loops);  // :169
+    if (rc) return rc;
+  }
+  const int rc = E.copy(P.uval, P.unew, E.n);  // :185
+  return rc ? rc : E.sync();
+}
+
 int DropletStepper::field(int which, double* out) {
   const DropMesh& M = P.mesh();
   const double* src[] = {M.d2ksi, M.d2eta, M.dksideta, M.J, M.A11, M.A22, M.A12, M.dksi, M.deta,

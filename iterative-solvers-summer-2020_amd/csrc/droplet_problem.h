@@ -54,6 +54,8 @@ class DropletStepper {
   int solve(double dt, double* U, nk_stats* st);             // :383 at the prepared mesh
   int pma(double dtm, int loops);                            // :384 / :589-599
   int step(double dt, double dtm, int loops, nk_stats* st, double* dt_used);  // :369-411
+  // initialise_coalescing_droplets (:132-189) from the current state
+  int init_coalescing(int vsteps, const DropSet& drops, double dtm, int loops);
   int field(int which, double* out);
   double scale = 1.0;
   nk_opts opts;

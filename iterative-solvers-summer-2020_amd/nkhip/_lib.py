@@ -49,7 +49,8 @@ class nk_drop_params(C.Structure):
                 ("endb", C.c_double), ("endt", C.c_double), ("epsilon", C.c_double),
                 ("n_exp", C.c_int32), ("m_exp", C.c_int32), ("Bo", C.c_double),
                 ("alpha2", C.c_double), ("alpha", C.c_double), ("gamma", C.c_double),
-                ("C", C.c_double), ("smoothing_iters", C.c_int32), ("pad_", C.c_int32)]
+                ("C", C.c_double), ("smoothing_iters", C.c_int32), ("pad_", C.c_int32),
+                ("a", C.c_double)]
 
 
 class nk_mems_params(C.Structure):
@@ -112,6 +113,7 @@ SIGNATURES = [
     ("nk_drop_residual", C.c_int, [_P, _P, _D, _P]),
     ("nk_drop_solve", C.c_int, [_P, _D, _P, C.POINTER(nk_stats)]),
     ("nk_drop_pma", C.c_int, [_P, _D, _I32]),
+    ("nk_drop_init_coalescing", C.c_int, [_P, _I32, C.POINTER(_D), _I32, _D, _I32]),
     ("nk_mems_params_default", C.c_int, [C.POINTER(nk_mems_params)]),
     ("nk_mems_create", C.c_int, [C.POINTER(_P), C.POINTER(nk_mems_params), C.POINTER(nk_opts),
                                  _P]),

@@ -115,6 +115,32 @@ class Droplet:
     def load_init(self, path):
         self.set_state(*read_init(path))
 
+    def initial_state(self):
+        """main() (:103-106): U = epsilon everywhere, Q = (xi^2 + eta^2)/2 on the grid."""
+        p = self.params
+        kk, ee = np.meshgrid(np.linspace(p.endl, p.endr, p.nx), np.linspace(p.endb, p.endt, p.ny))
+        return np.full(self.n, p.epsilon), np.reshape(0.5 * kk ** 2 + 0.5 * ee ** 2, self.n)
+
+    def initialise_coalescing(self, vsteps=1000, info=((0, 0, 1, 1), (3, 0, 1, 1)),
+                              dtmesh=5e-9, loops=20, tofile=None):
+        """initialise_coalescing_droplets(Vsteps, info, dtmesh, loops, False, tofile)
+        (droplet.py:132-189) from main()'s initial state: the droplets' volumes grow linearly
+        over `vsteps` steps, each followed by loop_pma(dtmesh, loops).  `tofile`: a directory to
+        write the reference's initdrop_coal_*.txt into (None: no file)."""
+        self.set_state(*self.initial_state())
+        rows = np.ascontiguousarray(np.asarray(info, dtype=np.float64).reshape(-1, 4))
+        check(lib.nk_drop_init_coalescing(
+            self._h, int(vsteps), rows.ctypes.data_as(C.POINTER(C.c_double)), rows.shape[0],
+            float(dtmesh), int(loops)), "nk_drop_init_coalescing")
+        U, Q = self.state()
+        if tofile is not None:
+            p = self.params
+            name = init_filename(R=1, Nx=p.nx, Ny=p.ny, a=int(p.a) if float(p.a).is_integer()
+                                 else p.a, epsilon=p.epsilon, alpha=p.alpha, gamma=p.gamma,
+                                 C_=p.C)
+            write_init(os.path.join(tofile, name), U.cpu().numpy(), Q.cpu().numpy())
+        return U, Q
+
     # ------------------------------------------------------------------ stepping
     def step(self, dt=1e-4, dtmesh=3e-9, pmaloops=400):
         """One iteration of evolve_with_PDE's loop (droplet.py:369-411)."""

@@ -26,7 +26,8 @@ P = SimpleNamespace(
     endl=-3.0, endr=6.0, endb=-3.0, endt=3.0,
     alpha=0.01, gamma=0.1, C=0.15,
     alpha2=0.0, n=6, m=3, Bo=0.01,
-)
+)  # a: droplet profile sharpness (:23)
+P.a = 100.0
 P.NN = P.Nx * P.Ny
 P.Dx = P.endr - P.endl
 P.Dy = P.endt - P.endb
@@ -324,3 +325,46 @@ def evolve(uval, qval, nsteps, dt=1e-4, dtmesh=3e-9, pmaloops=400, newton=None, 
         dts.append(dt_n)
         scale += np.exp(-10 * np.linalg.norm(u_new - uval))
     return u_new, qval, scale, dts
+
+
+# ------------------------------------------------------------ initialisation (droplet.py:132-189)
+def G2(xx, R):
+    """(:425-426)"""
+    return R + np.log((1 + np.exp(-2 * P.a * (xx + R))) / (1 + np.exp(-2 * P.a * (xx - R)))) / (2 * P.a)
+
+
+def H2(psi, R, V):
+    """(:428-429)"""
+    return 4 * V * (1 - psi * psi / (R * R)) / (R * R)
+
+
+def compute_U2(info, Q):
+    """compute_U2 (:413-423): precursor film plus one parabolic cap per (x, y, R, V) droplet,
+    evaluated at the physical node coordinates (Q.dksi, Q.deta)."""
+    ret = np.full(P.NN, P.epsilon)
+    for x, y, R, V in info:
+        ret += (1 - P.epsilon) * H2(G2(np.sqrt((Q.dksi - x) ** 2 + (Q.deta - y) ** 2), R), R, V)
+    return ret
+
+
+def initial_mesh():
+    """main() (:103): Q = (xi^2 + eta^2)/2, U = epsilon."""
+    kk, ee = np.meshgrid(np.linspace(P.endl, P.endr, P.Nx), np.linspace(P.endb, P.endt, P.Ny))
+    return np.full(P.NN, P.epsilon), np.reshape(0.5 * kk ** 2 + 0.5 * ee ** 2, P.NN)
+
+
+def init_coalescing(vsteps=1000, info=((0, 0, 1, 1), (3, 0, 1, 1)), dtmesh=5e-9, loops=20,
+                    unew=None, qval=None):
+    """initialise_coalescing_droplets (:132-189) without plotting or file I/O: inflate the
+    droplets' volumes linearly over `vsteps` steps, each followed by loop_pma(dtmesh, loops)."""
+    if unew is None:
+        unew, qval = initial_mesh()
+    vf = [d[3] for d in info]
+    for i in range(1, vsteps + 1):
+        uval = unew.copy()
+        Q = q_ders(qval)
+        U = u_ders(uval, Q)
+        arg = [(d[0], d[1], d[2], vf[k] * i / vsteps) for k, d in enumerate(info)]
+        unew = compute_U2(arg, Q)
+        qval = loop_pma(qval, uval, dtmesh, loops, Q=Q, U=U)
+    return unew, qval

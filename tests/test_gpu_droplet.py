@@ -79,3 +79,20 @@ def test_generic_dropin_on_droplet_residual(drop):
     U = nkhip.newton_krylov(lambda u: drop.residual(u, 1e-4), torch.as_tensor(U0, device="cuda"),
                             maxiter=20, f_tol=1e-7)
     assert np.abs(U.cpu().numpy() - z["U"]).max() <= 1e-7
+
+
+def test_initialise_coalescing_reproduces_reference_init_file(tmp_path):
+    """initialise_coalescing_droplets(1000, [[0,0,1,1],[3,0,1,1]], 5e-9, 20) -- 20 000 PMA loops
+    from the flat film -- against the reference's own initdrop_coal_1_91-61_... file (its output,
+    droplet.py:186-188).  Tolerance: 1e-10 relative (the NumPy oracle lands at 1.4e-12)."""
+    import nkhip
+    z = load_golden("droplet_init")
+    d = nkhip.Droplet()
+    try:
+        U, Q = d.initialise_coalescing(tofile=str(tmp_path))
+        assert _rel(U, z["U0"]) <= 1e-10
+        assert _rel(Q, z["Q0"]) <= 1e-12
+        U2, Q2 = nkhip.read_init(str(tmp_path / nkhip.droplet.init_filename()))
+        assert np.array_equal(U2, U.cpu().numpy()) and np.array_equal(Q2, Q.cpu().numpy())
+    finally:
+        d.close()

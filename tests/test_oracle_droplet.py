@@ -67,3 +67,12 @@ def test_init_file_roundtrip(tmp_path):
     U, Q = nkhip.read_init(p)
     assert np.array_equal(U, z["U0"]) and np.array_equal(Q, z["Q0"])
     assert os.path.basename(p) == "initdrop_coal_1_91-61_100_0.01_0.01_0.1_0.15.txt"
+
+
+def test_init_coalescing_reproduces_reference_init_file():
+    """The oracle's initialise_coalescing_droplets (droplet.py:132-189, 1000 x 20 PMA loops, about
+    a minute on one core) lands on the reference's own initdrop_coal_* output file."""
+    z = load_golden("droplet_init")
+    u, q = D.init_coalescing()
+    assert _rel(u, z["U0"]) <= 1e-11
+    assert _rel(q, z["Q0"]) <= 1e-13
