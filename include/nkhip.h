@@ -194,6 +194,20 @@ int nk_drop_pma(nk_drop* d, double dtmesh, int32_t loops);                      
 int nk_drop_init_coalescing(nk_drop* d, int32_t vsteps, const double* info, int32_t ndrops,
                             double dtmesh, int32_t loops);
 
+/* ---------------- semi-implicit SH step (python_work/sh_linearised.py) ----- */
+/* U[s+1] = solve(I + D - L k/2, (I + L k/2) U[s]), D = diag((5U[s] - U[s-1])^2 k/16 - g k U[s])
+ * (:48-56) on a periodic ny x nx grid of spacing h.  The reference factorises the sparse matrix
+ * (scipy spsolve); here a matrix-free conjugate-gradient solve on the 13-point stencil (the
+ * matrix is SPD whenever 1 + min D > k r/2, always for g = 0), warm-started from U[s], to
+ * |b - A x| <= rtol |b|.  Returns NK_NO_CONVERGENCE after maxiter iterations and NK_NONFINITE
+ * if p.Ap <= 0 (indefinite system) or the data are not finite. */
+typedef struct nk_shlin nk_shlin;
+int nk_shlin_create(nk_shlin** out, int64_t ny, int64_t nx, double h, double r, double g, double k,
+                    double rtol, int64_t maxiter, void* stream);
+int nk_shlin_destroy(nk_shlin* s);
+int nk_shlin_step(nk_shlin* s, const double* U_dev, const double* Uo_dev, double* Unew_dev,
+                  int64_t* iters, double* relres);
+
 /* ---------------- MEMS on a moving mesh (python_work/PMA2_nk.py) ------------ */
 /* u_t = -(-Lap)^2 u - lambda/(1+u)^2 + lambda eps^(m-2)/(1+u)^m on [endl, endr]^2 (N x N), one
  * PMA mesh step per time step.  Parameters = the module globals of PMA2_nk.py:22-37.  Only p = 2

@@ -14,6 +14,7 @@
 #include "droplet_problem.h"
 #include "mems_problem.h"
 #include "sh_problem.h"
+#include "shlin.h"
 
 using namespace nk;
 
@@ -434,6 +435,32 @@ int nk_drop_init_coalescing(nk_drop* d, int32_t vsteps, const double* info, int3
   for (int k = 0; k < ndrops; ++k)
     for (int c = 0; c < 4; ++c) D.v[k][c] = info[4 * k + c];
   return DS(d)->init_coalescing(vsteps, D, dtmesh, loops);
+}
+
+// ------------------------------------------------------------------------------ sh_linearised
+int nk_shlin_create(nk_shlin** out, int64_t ny, int64_t nx, double h, double r, double g, double k,
+                    double rtol, int64_t maxiter, void* stream) {
+  if (!out || ny < 5 || nx < 5 || !(h > 0) || !(k > 0) || !(rtol > 0) || maxiter < 1)
+    return NK_EINVAL;
+  std::unique_ptr<ShLinStepper> p(
+      new (std::nothrow) ShLinStepper(ny, nx, h, r, g, k, rtol, maxiter, S(stream), false));
+  if (!p) return NK_ENOMEM;
+  if (p->status()) return p->status();
+  *out = reinterpret_cast<nk_shlin*>(p.release());
+  return NK_OK;
+}
+int nk_shlin_destroy(nk_shlin* s) {
+  delete reinterpret_cast<ShLinStepper*>(s);
+  return NK_OK;
+}
+int nk_shlin_step(nk_shlin* s, const double* U, const double* Uo, double* Unew, int64_t* iters,
+                  double* relres) {
+  if (!s || !U || !Uo || !Unew) return NK_EINVAL;
+  ShLinStats st;
+  const int rc = reinterpret_cast<ShLinStepper*>(s)->step(U, Uo, Unew, &st);
+  if (iters) *iters = st.iters;
+  if (relres) *relres = st.relres;
+  return rc;
 }
 
 // ------------------------------------------------------------------------------ PMA2 (MEMS)

@@ -213,6 +213,38 @@ __global__ void __launch_bounds__(256) fddiff_kernel(double* w, const double* f0
   if (i < n) w[i] = (w[i] - f0[i]) / sc;
 }
 
+// CG update (sh_linearised's solve): x += alpha p; r -= alpha q; per-block sum of the new r^2.
+// Grid-stride over double2 pairs; one partial per block.
+template <bool VEC>
+__global__ void __launch_bounds__(256) cg_update_kernel(double* x, double* r, const double* p,
+                                                        const double* q, double alpha, int64_t n,
+                                                        double* partial) {
+  double acc[1] = {0.0};
+  const int64_t stride = 2 * int64_t(gridDim.x) * 256;
+  for (int64_t i = 2 * (int64_t(blockIdx.x) * 256 + threadIdx.x); i < n; i += stride) {
+    const double2 xv = ld2<VEC>(x, i, n), rv = ld2<VEC>(r, i, n);
+    const double2 pv = ld2<VEC>(p, i, n), qv = ld2<VEC>(q, i, n);
+    const double2 xn = make_double2(xv.x + alpha * pv.x, xv.y + alpha * pv.y);
+    const double2 rn = make_double2(rv.x - alpha * qv.x, rv.y - alpha * qv.y);
+    st2<VEC>(x, i, n, xn);
+    st2<VEC>(r, i, n, rn);
+    acc[0] += rn.x * rn.x;
+    if (i + 1 < n) acc[0] += rn.y * rn.y;
+  }
+  const double v = block_reduce<1, 1, 256>(acc);
+  if (threadIdx.x == 0) partial[blockIdx.x] = v;
+}
+
+// D of sh_linearised.py:50: d = (5U - Uo)(5U - Uo) k/16 - g k U
+__global__ void __launch_bounds__(256) shlin_diag_kernel(const double* U, const double* Uo,
+                                                         double k, double g, double* d,
+                                                         int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double a = 5 * U[i] - Uo[i];
+  d[i] = a * a * k / 16 - g * k * U[i];
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
@@ -286,6 +318,30 @@ hipError_t axpby_launch(double a, const double* x, double b, const double* y, do
   else
     hipLaunchKernelGGL(axpby_kernel<false>, dim3(unsigned(g)), dim3(256), 0, s, a, x, b, y, out,
                        n);
+  return hipGetLastError();
+}
+
+hipError_t cg_update_launch(double* x, double* r, const double* p, const double* q, double alpha,
+                            int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
+  const int64_t pairs = (n + 1) / 2;
+  int64_t g = (pairs + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  *nblk = g;
+  if (al16(x) && al16(r) && al16(p) && al16(q))
+    hipLaunchKernelGGL(cg_update_kernel<true>, dim3(unsigned(g)), dim3(256), 0, s, x, r, p, q,
+                       alpha, n, partial);
+  else
+    hipLaunchKernelGGL(cg_update_kernel<false>, dim3(unsigned(g)), dim3(256), 0, s, x, r, p, q,
+                       alpha, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t shlin_diag_launch(const double* U, const double* Uo, double k, double g, double* d,
+                             int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(shlin_diag_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, U, Uo, k,
+                     g, d, n);
   return hipGetLastError();
 }
 

@@ -36,6 +36,8 @@ enum class SMode : int {
   TRIAL = 4,  // w = a + alpha b: out2 = w, out1 = G(w), out0 = G(w) + p0; sums |F|^2, max|F|, max|w|
   FDJVP = 5,  // w = a + alpha b: out0 = (G(w) - p0) / sc          (_nonlin.py:1505-1513)
   AJVP = 6,   // out0 = alpha*(a/k - (L a + (2 g u - 3 u^2) a)/2) with u = p0 (analytic J v)
+  LINOP = 7,  // w = a + alpha b: out2 = w, out0 = (1 + p0) w - theta L w; sums w . out0
+              // (the semi-implicit operator I + D - L k/2 of sh_linearised.py:56, as CG's A p)
 };
 
 struct StencilArgs {
@@ -53,6 +55,7 @@ struct StencilArgs {
   // FDJVP/AJVP: if set, the step / scale come from the device value |z_raw|^2 (see jvp_scale)
   const double* znorm2 = nullptr;
   double omega = 0.0;
+  double theta = 0.0;  // LINOP
 };
 
 // Launches one stencil pass.  *nblk receives the number of partial-sum slots written (TRIAL).
@@ -92,6 +95,13 @@ hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, in
 // residual path (nk_solve) and of nk_axpy / nk_scal.
 // w = (w - f0) / sc, the finite difference of KrylovJacobian.matvec (_nonlin.py:1509).
 hipError_t fddiff_launch(double* w, const double* f0, double sc, int64_t n, hipStream_t s);
+// CG (sh_linearised): x += alpha p; r -= alpha q; partial[0..*nblk) = per-block sums of r'^2
+// (*nblk <= 1024).
+hipError_t cg_update_launch(double* x, double* r, const double* p, const double* q, double alpha,
+                            int64_t n, double* partial, hipStream_t s, int64_t* nblk);
+// d = (5U - Uo)^2 k/16 - g k U (sh_linearised.py:50)
+hipError_t shlin_diag_launch(const double* U, const double* Uo, double k, double g, double* d,
+                             int64_t n, hipStream_t s);
 hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
                         int64_t n, hipStream_t s);
 

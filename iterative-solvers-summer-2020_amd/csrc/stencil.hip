@@ -95,6 +95,9 @@ __device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const 
     r.o2 = na.c;
   } else if constexpr (M == SMode::FDJVP) {
     r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) / sc;
+  } else if constexpr (M == SMode::LINOP) {
+    r.o0 = (1.0 + pv) * na.c - A.theta * applyL(k, na);
+    r.o2 = na.c;
   } else {  // AJVP
     const double z = na.c, u = pv;
     r.o0 = alpha * (z / k.k - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
@@ -103,11 +106,14 @@ __device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const 
 }
 
 template <SMode M>
-constexpr bool kComb = (M == SMode::TRIAL || M == SMode::FDJVP);
+constexpr bool kComb = (M == SMode::TRIAL || M == SMode::FDJVP || M == SMode::LINOP);
+template <SMode M>
+constexpr bool kRed = (M == SMode::TRIAL || M == SMode::LINOP);
 template <SMode M>
 constexpr bool kTwo = (M == SMode::RESID);
 template <SMode M>
-constexpr bool kHasP0 = (M == SMode::TRIAL || M == SMode::FDJVP || M == SMode::AJVP);
+constexpr bool kHasP0 =
+    (M == SMode::TRIAL || M == SMode::FDJVP || M == SMode::AJVP || M == SMode::LINOP);
 template <SMode M>
 constexpr int kRad = (M == SMode::LAP5) ? 1 : 2;
 
@@ -236,6 +242,10 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
           red[1] = nmax(red[1], fabs(res[q].o0));
           red[2] = nmax(red[2], fabs(res[q].o2));
         }
+      } else if constexpr (M == SMode::LINOP) {
+        *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) red[0] += res[q].o2 * res[q].o0;
       }
     }
     // shift the window up by one row
@@ -253,7 +263,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
       if constexpr (kTwo<M>) wb[NR - 1][q] = nb_[q];
     }
   }
-  if constexpr (M == SMode::TRIAL) {
+  if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
     const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
     const int64_t bid = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
@@ -314,9 +324,12 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
       red[0] = res.o0 * res.o0;
       red[1] = fabs(res.o0);
       red[2] = fabs(res.o2);
+    } else if constexpr (M == SMode::LINOP) {
+      A.out2[idx] = res.o2;
+      red[0] = res.o2 * res.o0;
     }
   }
-  if constexpr (M == SMode::TRIAL) {
+  if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, 256>(red);
     if (threadIdx.x < 3) A.partial[threadIdx.x * int64_t(gridDim.x) + blockIdx.x] = v;
   }
@@ -382,6 +395,7 @@ hipError_t stencil_launch(SMode m, const StencilArgs& a, hipStream_t s, int64_t*
     case SMode::TRIAL: return launch_mode<SMode::TRIAL>(a, s, nblk);
     case SMode::FDJVP: return launch_mode<SMode::FDJVP>(a, s, nblk);
     case SMode::AJVP: return launch_mode<SMode::AJVP>(a, s, nblk);
+    case SMode::LINOP: return launch_mode<SMode::LINOP>(a, s, nblk);
   }
   return hipErrorInvalidValue;
 }
@@ -401,6 +415,7 @@ double stencil_bytes_per_point(SMode m, bool has_xt) {
     case SMode::TRIAL: return has_xt ? 48.0 : 40.0;  // read x, d, B; write F, G (, xt)
     case SMode::FDJVP: return 32.0;  // read x0, z, G0; write Jz
     case SMode::AJVP: return 24.0;   // read u, z; write Jz
+    case SMode::LINOP: return 40.0;  // read r, p, d; write p', A p
   }
   return 0.0;
 }

@@ -13,6 +13,7 @@ from .mems import Mems  # noqa: F401
 from .ops import (axpy, dot, lap5_apply, maxnorm, maxpy, mdot, nrm2, scal, sh13_apply,  # noqa: F401
                   sh_jvp, sh_residual)
 from .sh import SwiftHohenberg, sh_step  # noqa: F401
+from .shlin import SHLinearised  # noqa: F401
 from .solver import NoConvergence, newton_krylov  # noqa: F401
 
 __version__ = lib.nk_version().decode()

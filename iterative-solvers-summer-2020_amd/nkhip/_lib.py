@@ -114,6 +114,9 @@ SIGNATURES = [
     ("nk_drop_solve", C.c_int, [_P, _D, _P, C.POINTER(nk_stats)]),
     ("nk_drop_pma", C.c_int, [_P, _D, _I32]),
     ("nk_drop_init_coalescing", C.c_int, [_P, _I32, C.POINTER(_D), _I32, _D, _I32]),
+    ("nk_shlin_create", C.c_int, [C.POINTER(_P), _I64, _I64, _D, _D, _D, _D, _D, _I64, _P]),
+    ("nk_shlin_destroy", C.c_int, [_P]),
+    ("nk_shlin_step", C.c_int, [_P, _P, _P, _P, C.POINTER(_I64), C.POINTER(_D)]),
     ("nk_mems_params_default", C.c_int, [C.POINTER(nk_mems_params)]),
     ("nk_mems_create", C.c_int, [C.POINTER(_P), C.POINTER(nk_mems_params), C.POINTER(nk_opts),
                                  _P]),
