@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--n", type=int, default=4096, help="grid points per side")
     ap.add_argument("--jvp", choices=["fd", "analytic"], default="fd")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="testing: build the RCCL communicator even at world size 1")
     ap.add_argument("--extra", choices=["on", "off"], default="on",
                     help="also measure configs 2 (1024^2 Lap SpMV) and 3 (91x61 droplet)")
     return ap.parse_args()
@@ -176,7 +178,7 @@ def main():
             sys.exit(2)
     torch.cuda.set_device(local)
     comm = None
-    if world > 1:
+    if world > 1 or args.rccl_self:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         comm = nkhip.RcclComm.from_torch_distributed()
@@ -193,7 +195,7 @@ def main():
     a, b = U, torch.empty_like(U)
 
     def barrier():
-        if world > 1:
+        if world > 1 or args.rccl_self:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -285,7 +287,7 @@ def main():
     model.close()
     if comm is not None:
         comm.close()
-    if world > 1:
+    if world > 1 or args.rccl_self:
         dist.destroy_process_group()
 
 

@@ -42,7 +42,8 @@ __device__ __forceinline__ void st2(double* p, int64_t i, int64_t n, double2 v) 
 
 template <bool VEC>
 __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double* g, VecList P,
-                                                  int np, int64_t n, int cpb, double* partial) {
+                                                  int np, int64_t n, int cpb, double* partial,
+                                                  bool rev) {
   // One block walks `cpb` consecutive 2048-element chunks; per chunk the block keeps its slice of
   // a (and g) in registers and streams the vectors through it.  Per-vector block sums are
   // accumulated in LDS, so only one partial per block and value reaches HBM.
@@ -54,9 +55,11 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   const int wid = threadIdx.x >> 6;
   for (int t = lane; t < nv; t += 64) accw[wid][t] = 0.0;  // each wave zeroes its own slice
   double aa = 0.0;
+  const int64_t nchunks = (n + kKrylovChunk - 1) / kKrylovChunk;
   for (int c = 0; c < cpb; ++c) {
-    const int64_t chunk = bid * cpb + c;
-    if (chunk * kKrylovChunk >= n) break;  // uniform
+    const int64_t lc = bid * cpb + c;
+    if (lc >= nchunks) break;  // uniform
+    const int64_t chunk = rev ? nchunks - 1 - lc : lc;
     const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
     double2 av[PAIRS], gv[PAIRS];
 #pragma unroll
@@ -117,13 +120,15 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
 template <bool VEC>
 __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
                                                    VecList P, int np, int64_t n, int cpb,
-                                                   double* partial) {
+                                                   double* partial, bool rev) {
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
   double red[2] = {0.0, 0.0};
+  const int64_t nchunks = (n + kKrylovChunk - 1) / kKrylovChunk;
   for (int cc = 0; cc < cpb; ++cc) {
-    const int64_t chunk = bid * cpb + cc;
-    if (chunk * kKrylovChunk >= n) break;  // uniform
+    const int64_t lc = bid * cpb + cc;
+    if (lc >= nchunks) break;  // uniform
+    const int64_t chunk = rev ? nchunks - 1 - lc : lc;
     const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
     double2 acc[PAIRS];
 #pragma unroll
@@ -262,6 +267,14 @@ int64_t krylov_grid(int64_t n, int* cpb, int64_t target) {
   return (chunks + c - 1) / c;
 }
 
+bool traversal_reverse() {
+  static const bool on = env_int("NKHIP_PINGPONG", 1) != 0;
+  thread_local bool flip = false;
+  if (!on) return false;
+  flip = !flip;
+  return !flip;
+}
+
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
                        double* partial, hipStream_t s, int64_t* nblk) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
@@ -272,12 +285,13 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
   if (nb == 0) return hipSuccess;
   bool vec = al16(a) && al16(g);
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
+  const bool rev = traversal_reverse();
   if (vec)
     hipLaunchKernelGGL(mdot_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n, cpb,
-                       partial);
+                       partial, rev);
   else
     hipLaunchKernelGGL(mdot_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np, n, cpb,
-                       partial);
+                       partial, rev);
   return hipGetLastError();
 }
 
@@ -291,12 +305,13 @@ hipError_t combo_launch(double* out, const double* in, double cin, const VecList
   if (nb == 0) return hipSuccess;
   bool vec = al16(out) && al16(in);
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
+  const bool rev = traversal_reverse();
   if (vec)
     hipLaunchKernelGGL(combo_kernel<true>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
-                       np, n, cpb, partial);
+                       np, n, cpb, partial, rev);
   else
     hipLaunchKernelGGL(combo_kernel<false>, dim3(unsigned(nb)), dim3(BS), 0, s, out, in, cin, P,
-                       np, n, cpb, partial);
+                       np, n, cpb, partial, rev);
   return hipGetLastError();
 }
 

@@ -56,7 +56,14 @@ struct StencilArgs {
   const double* znorm2 = nullptr;
   double omega = 0.0;
   double theta = 0.0;  // LINOP
+  bool rev = false;    // set by stencil_launch (traversal_reverse)
 };
+
+// MALL-friendly ping-pong: successive streaming kernels launched from one host thread alternate
+// their traversal direction, so each starts on the address range its predecessor touched last
+// (up to 256 MB of which may still sit in the memory-side Infinity Cache).  Flips on every call;
+// NKHIP_PINGPONG=0 keeps every kernel forward.
+bool traversal_reverse();
 
 // Launches one stencil pass.  *nblk receives the number of partial-sum slots written (TRIAL).
 hipError_t stencil_launch(SMode m, const StencilArgs& a, hipStream_t s, int64_t* nblk);

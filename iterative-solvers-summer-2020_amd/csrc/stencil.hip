@@ -181,9 +181,11 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   // time (both at their start or both at their end), so the halo rows one band re-reads are still
   // in L2.  The window sums below pair the rows symmetrically about the centre, so the result is
   // bitwise the same in either direction (fp addition is commutative).
-  const int64_t r0 = int64_t(blockIdx.y) * RY;
+  // A.rev walks the bands from the top of the grid (see traversal_reverse)
+  const int64_t band = A.rev ? int64_t(gridDim.y) - 1 - blockIdx.y : int64_t(blockIdx.y);
+  const int64_t r0 = band * RY;
   const int64_t r1 = (r0 + RY < ny) ? r0 + RY : ny;
-  const bool up = (blockIdx.y & 1) != 0;
+  const bool up = (band & 1) != 0;
   const int64_t dir = up ? -1 : 1;
   const int64_t rs = up ? r1 - 1 : r0;
 #pragma unroll
@@ -372,6 +374,7 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     const int64_t gy = (A.ny + RY - 1) / RY;
     if (gy > 65535) return hipErrorInvalidValue;
     if (nblk) *nblk = gx * gy;
+    B.rev = traversal_reverse();
     hipLaunchKernelGGL((march_kernel<M, BX>), dim3(unsigned(gx), unsigned(gy)), dim3(BX), 0, s, B,
                        RY);
   } else {

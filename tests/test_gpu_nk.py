@@ -165,3 +165,45 @@ def test_large_grid_root_property():
     F = sh_oracle.residual(U1.cpu().numpy().reshape(-1), U0.reshape(-1), N, N, 0.625, 0.01, 0.2,
                            1.0)
     assert np.abs(F).max() <= 6.06e-6 * 1.01
+
+
+def test_rccl_world1_matches_single_slab():
+    """The RCCL communicator path on one GPU: ncclCommInitRank, the grouped halo send/recv (to
+    itself, prev == next == 0) and the in-stream all-reduces, against the plain periodic slab."""
+    import nkhip
+    N = 96
+    U0 = np.random.default_rng(2020).standard_normal((N, N))
+    single = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10)
+    ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+    single.close()
+    comm = nkhip.RcclComm.create(nkhip.RcclComm.unique_id(), 0, 1)
+    try:
+        m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comm, ny_local=N)
+        got = m.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+        m.close()
+    finally:
+        comm.close()
+    assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
+
+
+def test_rccl_from_torch_distributed_world1():
+    """bench.py's multi-GPU bring-up (nccl process group, unique id broadcast) at world size 1."""
+    import os
+    import torch.distributed as dist
+    import nkhip
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        comm = nkhip.RcclComm.from_torch_distributed()
+        N = 64
+        U0 = np.random.default_rng(3).standard_normal((N, N))
+        m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, comm=comm, ny_local=N)
+        got = m.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+        m.close()
+        comm.close()
+        ref = nkhip.SwiftHohenberg(N=N, d=0.625 * N).step(torch.as_tensor(U0, device="cuda"))
+        assert np.abs(got - ref.cpu().numpy()).max() <= 1e-8 * max(1.0, np.abs(got).max())
+    finally:
+        dist.destroy_process_group()
