@@ -152,6 +152,94 @@ def config3_droplet(steps=5, cpu_steps=2):
             "pma_loops_per_step": 400}
 
 
+def config_pma2(steps=20, cpu_steps=2):
+    """the PMA2 MEMS moving-mesh stepper (PMA2_nk.py main() loop, 51^2, one PMA
+    mesh step + one Newton-Krylov solve per time step), GPU vs the restated reference path."""
+    import torch
+
+    import nkhip
+    from oracle import pma2_oracle
+    m = nkhip.Mems()
+    m.step()  # warm-up
+    m.set_state(*m.initial_state())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nit = 0
+    for _ in range(steps):
+        m.step()
+        nit += m.last_stats["nit"]
+    torch.cuda.synchronize()
+    gpu = time.perf_counter() - t0
+    m.close()
+    u, q = pma2_oracle.initial_state()
+    t0 = time.perf_counter()
+    for _ in range(cpu_steps):
+        u, q, _ = pma2_oracle.step(u, q)
+    cpu = time.perf_counter() - t0
+    return {"workload": "pma2_mems_51x51_step", "steps": steps,
+            "gpu_steps_per_s": round(steps / gpu, 2), "newton_its_per_step": nit / steps,
+            "cpu_reference_path_steps_per_s": round(cpu_steps / cpu, 3), "cpu_steps": cpu_steps}
+
+
+def config_shlin(sizes=((64, 30, 30), (512, 20, 2))):
+    """sh_linearised.py's semi-implicit step (r = 0.2, g = 0, k = 0.2,
+    h = 0.625): GPU matrix-free CG vs the reference's scipy spsolve on the assembled matrix."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    from oracle import shlin_oracle
+    from oracle.sh_oracle import csr_L
+    out = {}
+    for n, steps, cpu_steps in sizes:
+        U0 = np.random.default_rng(2020).standard_normal(n * n)
+        s = nkhip.SHLinearised(N=n, d=0.625 * n, k=0.2, r=0.2, g=0.0)
+        U = torch.as_tensor(U0, device="cuda")
+        s.step(U, U)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Uo, its = U, 0
+        for _ in range(steps):
+            U, Uo = s.step(U, Uo), U
+            its += s.last_iters
+        torch.cuda.synchronize()
+        gpu = time.perf_counter() - t0
+        s.close()
+        L = csr_L(n, 0.625, 0.2).tocsc()
+        t0 = time.perf_counter()
+        u, uo = U0.copy(), U0.copy()
+        for _ in range(cpu_steps):
+            u, uo = shlin_oracle.step(L, u, uo, 0.2, 0.0), u
+        cpu = time.perf_counter() - t0
+        out[f"{n}x{n}"] = {"gpu_steps_per_s": round(steps / gpu, 2),
+                           "cg_iters_per_step": its / steps,
+                           "cpu_spsolve_steps_per_s": round(cpu_steps / cpu, 3)}
+    return {"workload": "sh_linearised_semi_implicit_step", **out}
+
+
+def config_droplet_init():
+    """initialise_coalescing_droplets(1000, [[0,0,1,1],[3,0,1,1]], 5e-9, 20) on
+    the GPU (20 000 PMA loops); checked against the reference's initdrop_coal_* file."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    with np.load(os.path.join(ROOT, "tests", "golden", "droplet_init.npz")) as z:
+        U0 = z["U0"]
+    d = nkhip.Droplet()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    U, _ = d.initialise_coalescing()
+    torch.cuda.synchronize()
+    gpu = time.perf_counter() - t0
+    d.close()
+    err = float(np.abs(U.cpu().numpy() - U0).max() / np.abs(U0).max())
+    return {"workload": "droplet_initialise_coalescing_1000x20", "gpu_s": round(gpu, 3),
+            "rel_err_vs_reference_init_file": err,
+            "cpu_reference_path_s": "64.3 (NumPy restatement, one core, measured in the build "
+                                    "container; tests/test_oracle_droplet.py)"}
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "latest_traffic.json")
     try:
@@ -282,7 +370,9 @@ def main():
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
             out["cpu_baseline"] = cpu_baseline(n, h, k, r, g, fe)
         if world == 1 and args.extra == "on":
-            out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet()}
+            out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet(),
+                                    "pma2": config_pma2(), "sh_linearised": config_shlin(),
+                                    "droplet_init": config_droplet_init()}
         print(json.dumps(out), flush=True)
     model.close()
     if comm is not None:
