@@ -57,6 +57,7 @@ struct StencilArgs {
   double omega = 0.0;
   double theta = 0.0;  // LINOP
   bool rev = false;    // set by stencil_launch (traversal_reverse)
+  bool nt_p0 = false;  // set by stencil_launch: non-temporal loads of the point-wise input
 };
 
 // MALL-friendly ping-pong: successive streaming kernels launched from one host thread alternate

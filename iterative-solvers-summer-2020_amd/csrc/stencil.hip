@@ -139,6 +139,17 @@ __device__ __forceinline__ void jvp_scale(const StencilArgs& A, double* alpha, d
   }
 }
 
+// The point-wise input (G0, B, u or D) is streamed once per pass: optionally non-temporal, so it
+// does not evict the stencil fields from L2 / the Infinity Cache.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld_p0(const StencilArgs& A, const double* p) {
+  if (A.nt_p0) {
+    const dv2 v = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p));
+    return make_double2(v.x, v.y);
+  }
+  return *reinterpret_cast<const double2*>(p);
+}
+
 // ------------------------------------------------------------------------------------------
 // march kernel
 // ------------------------------------------------------------------------------------------
@@ -195,7 +206,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   // the point-wise input is prefetched one row ahead as well, so that the compute of row r waits
   // only for loads issued during the previous iteration (in-order vmcnt)
   double2 pv_next = make_double2(0.0, 0.0);
-  if constexpr (kHasP0<M>) pv_next = *reinterpret_cast<const double2*>(A.p0 + rs * nx + cc);
+  if constexpr (kHasP0<M>) pv_next = ld_p0(A, A.p0 + rs * nx + cc);
   for (int64_t it = 0; it < r1 - r0; ++it) {
     const int64_t r = rs + dir * it;
     const int64_t o = r * nx + cc;
@@ -203,7 +214,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
     if constexpr (kHasP0<M>) {
       int64_t rp = r + dir;
       rp = (rp >= ny) ? ny - 1 : ((rp < 0) ? 0 : rp);
-      pv_next = *reinterpret_cast<const double2*>(A.p0 + rp * nx + cc);
+      pv_next = ld_p0(A, A.p0 + rp * nx + cc);
     }
     // prefetch the next entering row (unconditionally: past the band end it re-reads a valid
     // halo row, which keeps the load count per iteration fixed for the waitcnt schedule)
@@ -361,11 +372,12 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
         f->hi = f->base;
       }
     }
-    // Row band per block: aim for >= ~2048 blocks (8 per CU) with bands of 4..32 rows.
+    // Row band per block: aim for >= ~4096 blocks (16 per CU) with bands of 4..32 rows
+    // (4096^2: RY = 16, measured best of 8..256).
     // (NKHIP_RY_MIN / NKHIP_RY_MAX / NKHIP_BLOCKS override the choice for tuning runs.)
     static const int ry_min = env_int("NKHIP_RY_MIN", 4);
     static const int ry_max = env_int("NKHIP_RY_MAX", 32);
-    static const int blocks = env_int("NKHIP_BLOCKS", 2048);
+    static const int blocks = env_int("NKHIP_BLOCKS", 4096);
     constexpr int BX = 128;
     const int64_t gx = (A.nx / 2 + BX - 1) / BX;
     int64_t ry = (A.ny * gx) / blocks;
@@ -375,6 +387,8 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     if (gy > 65535) return hipErrorInvalidValue;
     if (nblk) *nblk = gx * gy;
     B.rev = traversal_reverse();
+    static const bool nt_p0 = env_int("NKHIP_NT_P0", 1) != 0;
+    B.nt_p0 = nt_p0;
     hipLaunchKernelGGL((march_kernel<M, BX>), dim3(unsigned(gx), unsigned(gy)), dim3(BX), 0, s, B,
                        RY);
   } else {

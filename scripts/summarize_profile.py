@@ -73,6 +73,7 @@ def main():
     print("\n".join(out))
     # per-kernel-class HBM traffic per launch (PMC) next to the algorithmic bytes of the SAME run
     classes = {"combo_kernel<true>": "krylov_combo", "mdot_kernel<true>": "krylov_mdot",
+               "combo_kernel<true, true>": "krylov_combo", "mdot_kernel<true, true>": "krylov_mdot",
                "march_kernel<(nk::SMode)5, 128>": "sh_fdjvp",
                "march_kernel<(nk::SMode)6, 128>": "sh_ajvp",
                "march_kernel<(nk::SMode)4, 128>": "sh_trial",
