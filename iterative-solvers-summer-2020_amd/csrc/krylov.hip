@@ -186,22 +186,30 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
   }
 }
 
-__global__ void __launch_bounds__(256) reduce_final_kernel(const double* partial, int64_t nblk,
-                                                           int nsum, double* result,
-                                                           double* result_host) {
+constexpr int RB = 1024;  // reduce_final block: <= 4 partials per thread at 4096 producer blocks
+
+__global__ void __launch_bounds__(RB) reduce_final_kernel(const double* partial, int64_t nblk,
+                                                          int nsum, double* result,
+                                                          double* result_host) {
   const int k = blockIdx.x;
   const bool is_sum = k < nsum;
   const double* p = partial + int64_t(k) * nblk;
-  // max reductions start from -inf (signed quantities such as -min(...) are allowed)
+  // max reductions start from -inf (signed quantities such as -min(...) are allowed); the
+  // loads of one thread are issued together (no dependent load chain)
   double acc = is_sum ? 0.0 : -INFINITY;
-  for (int64_t b = threadIdx.x; b < nblk; b += 256) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
+  int64_t b = threadIdx.x;
+  for (; b + 3 * RB < nblk; b += 4 * RB) {
+    const double x0 = p[b], x1 = p[b + RB], x2 = p[b + 2 * RB], x3 = p[b + 3 * RB];
+    acc = is_sum ? acc + x0 + x1 + x2 + x3 : nmax(nmax(nmax(nmax(acc, x0), x1), x2), x3);
+  }
+  for (; b < nblk; b += RB) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
   double v[1] = {acc};
   // the reduction tree is fixed, so the result does not depend on timing
   double s = 0.0;
   if (is_sum) {
-    s = block_reduce<1, 1, 256>(v);
+    s = block_reduce<1, 1, RB>(v);
   } else {
-    s = block_reduce<1, 0, 256>(v);
+    s = block_reduce<1, 0, RB>(v);
   }
   if (nblk == 0) s = 0.0;  // empty input
   if (threadIdx.x == 0) {
@@ -339,7 +347,7 @@ hipError_t combo_launch(double* out, const double* in, double cin, const VecList
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,
                                double* result, double* result_host, hipStream_t s) {
   if (nv <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reduce_final_kernel, dim3(unsigned(nv)), dim3(256), 0, s, partial, nblk, nsum,
+  hipLaunchKernelGGL(reduce_final_kernel, dim3(unsigned(nv)), dim3(RB), 0, s, partial, nblk, nsum,
                      result, result_host);
   return hipGetLastError();
 }
