@@ -125,7 +125,8 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
       return combo_launch(w, w, 1.0, U, j + 1, n, E_.partial(), E_.s, &nblk);
     });
-    if (!rc) rc = E_.reduce_async(nblk, 1, 2, Engine::kSlotCombo);
+    // only |v_{j+1}|^2 is used (a non-finite v shows up in it): one sum, one all-reduce on N GPUs
+    if (!rc) rc = E_.reduce_async(nblk, 1, 1, Engine::kSlotCombo);
     if (rc) return rc;
     // -- speculatively start step j+1 when its direction is v_{j+1} (device-side JVP scale)
     const bool more = j + 1 < m;

@@ -137,7 +137,8 @@ int Engine::copy(double* dst, const double* src, int64_t cnt) {
 
 int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot) {
   if (slot < 0 || slot + nv > kReduceSlots) return NK_EINVAL;
-  const bool multi = comm && comm->size() > 1;
+  // any communicator (also a world of one) takes the all-reduce path
+  const bool multi = comm != nullptr;
   int rc = launch(K_REDUCE, 8.0 * nblk * nv, [&] {
     return reduce_final_launch(partial_, nblk, nsum, nv, dres_ + slot,
                                multi ? nullptr : hres_ + slot, s);

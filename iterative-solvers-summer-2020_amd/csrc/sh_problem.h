@@ -28,9 +28,12 @@ class SHProblem final : public Problem {
   int set_dir(const double* d) override;
 
  private:
-  bool dist() const { return E_.comm && E_.comm->size() > 1; }
+  // any communicator (also a world of one: its halo is the periodic wrap through RCCL)
+  bool dist() const { return E_.comm != nullptr; }
   Field field(const double* p, const double* halo) const;
   int halo(const double* v, double* h);
+  // the JVP pass on a slab: halo of z + stencil; interior rows overlap the exchange
+  int halo_stencil(int kind, SMode m, const StencilArgs& A, const double* z, double* zh);
   Engine& E_;
   int64_t ny_, nx_, ny_g_;
   SHCoef c_;
@@ -41,6 +44,8 @@ class SHProblem final : public Problem {
   double* hz_ = nullptr;
   double* hd_ = nullptr;
   double* hu_ = nullptr;
+  hipStream_t side_ = nullptr;       // interior rows of the JVP while the halo is in flight
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):
