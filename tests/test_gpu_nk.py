@@ -115,11 +115,12 @@ def test_deterministic_runs():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 4])
-def test_loopback_slabs_match_single_slab(nranks):
-    """The row-slab decomposition (halo exchange + all-reduce) on one GPU, one thread per slab."""
+@pytest.mark.parametrize("nranks,N", [(2, 96), (3, 96), (4, 96), (2, 61), (1, 64)])
+def test_loopback_slabs_match_single_slab(nranks, N):
+    """The row-slab decomposition (halo exchange + all-reduce) on one GPU, one thread per slab;
+    N = 61 takes the point kernel (odd nx) through the interior/edge split, nranks = 1 the
+    periodic wrap through the communicator."""
     import nkhip
-    N = 96
     U0 = np.random.default_rng(2020).standard_normal((N, N))
     single = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10)
     ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
