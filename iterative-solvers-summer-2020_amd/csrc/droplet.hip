@@ -181,22 +181,32 @@ __device__ __forceinline__ double pressure(const DropParams& P, double h, double
 // operator takes its 5-point interior form) first, branch-free (kIn = true), then the 3-wide
 // boundary ring with the general per-position code.  Only the one wave straddling the split
 // diverges; a row-major walk would put boundary columns in nearly every wave.
+// Division by a run-time divisor d as one multiply-high: q = umulhi(t, ceil(2^32/d)), exact
+// while t*d < 2^32 (shape_ok bounds the grid so).
+struct FastDiv {
+  uint32_t m;
+  __device__ explicit FastDiv(uint32_t d) : m(0xFFFFFFFFu / d + 1u) {}
+  __device__ int operator()(int t) const { return int(__umulhi(uint32_t(t), m)); }
+};
+
 template <class F>
 __device__ __forceinline__ void for_points(int nx, int ny, F f) {
   const int ix = nx - 6, iy = ny - 6, nI = ix * iy, NN = nx * ny;
+  const FastDiv dix(ix), diy(iy), dnx(nx);
   for (int t = threadIdx.x; t < NN; t += DB) {
     if (t < nI) {
-      const int i = 3 + t / ix, j = 3 + t % ix;
+      const int q = dix(t);
+      const int i = 3 + q, j = 3 + (t - q * ix);
       f(i * nx + j, i, j, std::true_type{});
     } else {
       int u = t - nI, i, j;
       if (u < 6 * nx) {  // rows 0-2 and ny-3..ny-1
-        const int r = u / nx;
+        const int r = dnx(u);
         i = r < 3 ? r : ny - 6 + r;
         j = u - r * nx;
       } else {  // columns 0-2 and nx-3..nx-1 of rows 3..ny-4
         u -= 6 * nx;
-        const int c = u / iy;
+        const int c = diy(u);
         j = c < 3 ? c : nx - 6 + c;
         i = 3 + (u - c * iy);
       }
@@ -872,7 +882,11 @@ Coefs make_coefs(const DropParams& P) {
   return C;
 }
 
-bool shape_ok(const DropParams& P) { return P.nx >= 7 && P.ny >= 7; }
+// >= 7 points per side (3-wide boundary ring + interior); FastDiv exact: NN * max(nx, ny) < 2^32
+bool shape_ok(const DropParams& P) {
+  return P.nx >= 7 && P.ny >= 7 &&
+         double(P.nx) * P.ny * (P.nx > P.ny ? P.nx : P.ny) < 4294967295.0;
+}
 
 }  // namespace
 
