@@ -49,7 +49,8 @@ typedef struct nk_opts {
   int32_t line_search; /* 1 = 'armijo' (default), 0 = None */
   int32_t jvp_mode;    /* NK_JVP_FD (default) or NK_JVP_ANALYTIC */
   int32_t verbose;     /* print "%d:  |F(x)| = %g; step %g" per Newton iteration */
-  int32_t profile;     /* record HIP events around every kernel (see nk_sh_kernel_profile) */
+  int32_t profile;     /* 0: off; k >= 1: time every k-th launch of each kernel class with HIP
+                          events (see nk_sh_kernel_profile; each event pair costs ~5 us) */
 } nk_opts;
 
 typedef struct nk_stats {
@@ -66,9 +67,11 @@ typedef struct nk_stats {
 /* Per-kernel-class timings recorded with HIP events on the solver's stream. */
 typedef struct nk_kprof {
   char name[32];
-  int64_t launches;
-  double total_ms;
-  double alg_bytes;    /* algorithmic HBM bytes summed over launches */
+  int64_t launches;    /* all launches */
+  double total_ms;     /* summed duration of the timed launches */
+  double alg_bytes;    /* algorithmic HBM bytes summed over all launches */
+  int64_t timed;       /* launches timed (every opts.profile-th) */
+  double timed_bytes;  /* algorithmic HBM bytes of the timed launches */
 } nk_kprof;
 
 typedef struct nk_comm nk_comm;

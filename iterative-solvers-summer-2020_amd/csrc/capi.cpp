@@ -236,8 +236,9 @@ int nk_sh_create(nk_sh** out, int64_t ny_local, int64_t nx, int64_t ny_global, d
   sh->opts = opts ? *opts : default_opts();
   sh->ny = ny_local;
   sh->nx = nx;
-  sh->E = std::make_unique<Engine>(ny_local * nx, comm, S(stream), sh->opts.profile != 0,
+  sh->E = std::make_unique<Engine>(ny_local * nx, comm, S(stream), sh->opts.profile > 0,
                                    stencil_partial_slots(ny_local, nx));
+  sh->E->sample = sh->opts.profile > 1 ? sh->opts.profile : 1;
   sh->P = std::make_unique<SHProblem>(*sh->E, ny_local, nx, ny_global, sh_coef(h, r, k, g),
                                       sh->opts.jvp_mode);
   if (sh->P->status()) return sh->P->status();
@@ -258,7 +259,8 @@ int nk_sh_set_opts(nk_sh* s, const nk_opts* opts) {
   if (!s || !opts) return NK_EINVAL;
   if (opts->inner_m != s->opts.inner_m || opts->outer_k != s->opts.outer_k) return NK_EINVAL;
   s->opts = *opts;
-  s->E->profile = opts->profile != 0;
+  s->E->profile = opts->profile > 0;
+  s->E->sample = opts->profile > 1 ? opts->profile : 1;
   s->P->set_jvp_mode(opts->jvp_mode);
   s->NK->set_opts(*opts);
   return NK_OK;
@@ -282,6 +284,8 @@ int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {
     out[k].launches = s->E->stat(k).launches;
     out[k].total_ms = s->E->stat(k).ms;
     out[k].alg_bytes = s->E->stat(k).bytes;
+    out[k].timed = s->E->stat(k).timed;
+    out[k].timed_bytes = s->E->stat(k).tbytes;
   }
   return K_NKINDS;
 }

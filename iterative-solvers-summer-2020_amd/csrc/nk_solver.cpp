@@ -109,9 +109,9 @@ void Engine::harvest() {
   for (auto& p : pend_) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, p.a, p.b);
-    stats_[p.kind].launches += 1;
+    stats_[p.kind].timed += 1;
     stats_[p.kind].ms += ms;
-    stats_[p.kind].bytes += p.bytes;
+    stats_[p.kind].tbytes += p.bytes;
     free_ev_.push_back(p.a);
     free_ev_.push_back(p.b);
   }
@@ -120,6 +120,7 @@ void Engine::harvest() {
 
 void Engine::reset_stats() {
   for (auto& k : stats_) k = KStat{};
+  for (auto& t : tick_) t = 0;
 }
 
 int Engine::sync() {

@@ -41,7 +41,7 @@ class nk_stats(C.Structure):
 
 class nk_kprof(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
-                ("alg_bytes", C.c_double)]
+                ("alg_bytes", C.c_double), ("timed", C.c_int64), ("timed_bytes", C.c_double)]
 
 
 class nk_drop_params(C.Structure):

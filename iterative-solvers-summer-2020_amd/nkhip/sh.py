@@ -128,7 +128,8 @@ class SwiftHohenberg:
         recs = (_lib.nk_kprof * 16)()
         n = check(lib.nk_sh_kernel_profile(self._h, recs, 16), "nk_sh_kernel_profile")
         return {recs[i].name.decode(): {"launches": recs[i].launches, "ms": recs[i].total_ms,
-                                        "alg_bytes": recs[i].alg_bytes} for i in range(n)}
+                                        "alg_bytes": recs[i].alg_bytes, "timed": recs[i].timed,
+                                        "timed_bytes": recs[i].timed_bytes} for i in range(n)}
 
     def reset_profile(self):
         check(lib.nk_sh_reset_profile(self._h), "nk_sh_reset_profile")

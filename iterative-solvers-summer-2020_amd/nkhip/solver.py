@@ -60,7 +60,8 @@ def make_opts(*, rdiff=None, inner_maxiter=20, outer_k=10, verbose=False, maxite
         raise ValueError("jvp must be 'fd' (scipy-faithful) or 'analytic'")
     o.jvp_mode = _lib.NK_JVP_FD if jvp == "fd" else _lib.NK_JVP_ANALYTIC
     o.verbose = 1 if verbose else 0
-    o.profile = 1 if profile else 0
+    # profile: False/0 off, True/1 every launch timed, k > 1 every k-th launch of each class
+    o.profile = int(profile) if not isinstance(profile, bool) else (1 if profile else 0)
     # inner_maxiter is the LGMRES outer-cycle count, which KrylovJacobian overrides to 1
     # (_nonlin.py:1483), so it has no effect -- accepted for signature compatibility.
     del inner_maxiter

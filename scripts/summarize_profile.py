@@ -88,7 +88,8 @@ def main():
                "hbm_write_bytes_per_launch": w[1] * 1024 / w[0]}
         if bench and cls in bench.get("kernels", {}):
             kb = bench["kernels"][cls]
-            alg = kb["GB/s"] * 1e9 * kb["ms"] * 1e-3 / kb["launches"]
+            alg = (kb["alg_MB_per_launch"] * 1e6 if "alg_MB_per_launch" in kb
+                   else kb["GB/s"] * 1e9 * kb["ms"] * 1e-3 / kb["launches"])
             rec["alg_bytes_per_launch"] = alg
             rec["traffic_over_alg"] = (rec["hbm_read_bytes_per_launch"]
                                        + rec["hbm_write_bytes_per_launch"]) / alg
