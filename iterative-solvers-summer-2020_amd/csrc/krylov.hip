@@ -68,11 +68,12 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   const int wid = threadIdx.x >> 6;
   for (int t = lane; t < nv; t += 64) accw[wid][t] = 0.0;  // each wave zeroes its own slice
   double aa = 0.0;
-  const int64_t nchunks = (n + kKrylovChunk - 1) / kKrylovChunk;
+  // rev: the blocks dispatched first take the last chunk groups; a group's chunks, their order and
+  // its partial slot do not depend on rev, so the sums are bitwise the same in both directions
+  const int64_t grp = rev ? nblk - 1 - bid : bid;
   for (int c = 0; c < cpb; ++c) {
-    const int64_t lc = bid * cpb + c;
-    if (lc >= nchunks) break;  // uniform
-    const int64_t chunk = rev ? nchunks - 1 - lc : lc;
+    const int64_t chunk = grp * cpb + c;
+    if (chunk * kKrylovChunk >= n) break;  // uniform
     const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
     double2 av[PAIRS], gv[PAIRS];
 #pragma unroll
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
     double v = accw[0][k];
 #pragma unroll
     for (int w = 1; w < BS / 64; ++w) v += accw[w][k];
-    partial[int64_t(k) * nblk + bid] = v;
+    partial[int64_t(k) * nblk + grp] = v;
   }
 }
 
@@ -137,11 +138,10 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
   double red[2] = {0.0, 0.0};
-  const int64_t nchunks = (n + kKrylovChunk - 1) / kKrylovChunk;
+  const int64_t grp = rev ? nblk - 1 - bid : bid;  // see mdot_kernel
   for (int cc = 0; cc < cpb; ++cc) {
-    const int64_t lc = bid * cpb + cc;
-    if (lc >= nchunks) break;  // uniform
-    const int64_t chunk = rev ? nchunks - 1 - lc : lc;
+    const int64_t chunk = grp * cpb + cc;
+    if (chunk * kKrylovChunk >= n) break;  // uniform
     const int64_t base = chunk * kKrylovChunk + 2 * int64_t(threadIdx.x);
     double2 acc[PAIRS];
 #pragma unroll
@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
   }
   if (partial) {
     const double v = block_reduce<2, 1, BS>(red);
-    if (threadIdx.x < 2) partial[int64_t(threadIdx.x) * nblk + bid] = v;
+    if (threadIdx.x < 2) partial[int64_t(threadIdx.x) * nblk + grp] = v;
   }
 }
 

@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
     const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
-    const int64_t bid = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
+    const int64_t bid = band * gridDim.x + blockIdx.x;  // slot by band: independent of A.rev
     if (threadIdx.x < 3) A.partial[threadIdx.x * nblk + bid] = v;
   }
 }
