@@ -2,14 +2,25 @@
 // (x0 = 0, maxiter = 1, M = identity, prepend_outer_v = True, store_outer_Av = False) around the
 // FGMRES Arnoldi process of scipy/sparse/linalg/_isolve/_gcrotmk.py:14-180.
 //
-// Device/host split per Arnoldi step j (one host synchronisation per step):
+// Device/host split per Arnoldi step j -- one host synchronisation and ONE reduction (one
+// all-reduce on N GPUs) per step:
 //   host   h_j from the multi-dot of step j:  (I + L) h = V^T w_j  (inverse compact-WY MGS)
-//   device combo_j:  v_{j+1} = w_j - V h_j,  |v_{j+1}|^2          -> device slot
-//   device JVP_{j+1}(v_{j+1}) with its step taken from that device slot, then multi-dot_{j+1}
-//   sync   host finishes step j (Givens QR of the Hessenberg column, residual test).
-// When step j turns out to be the last one, the JVP/multi-dot issued for j+1 are discarded.
+//   device combo_j:  v_{j+1} = tau w_j - V h_j  (no reduction)
+//   device JVP_{j+1} of v_{j+1} / |v_{j+1}|_est, with |v_{j+1}|_est^2 = |w_j|^2 - |h_j|^2 (the
+//          Pythagoras identity of the Gram-Schmidt step, exact in exact arithmetic)
+//   device multi-dot_{j+1}: V^T w_{j+1}, the Gram row of v_{j+1} INCLUDING |v_{j+1}|^2, |w_{j+1}|^2
+//   sync   host finishes step j with the exact |v_{j+1}| from that Gram diagonal (Givens QR of the
+//          Hessenberg column, residual test) and rescales w_{j+1} by tau = |v|_est / |v|: the JVP
+//          was applied to a vector of norm 1 +- rounding, as in KrylovJacobian.matvec, so
+//          tau * w_{j+1} = J v_{j+1} with the exactly normalised v_{j+1}.
+// When |v_{j+1}| << |w_j| the estimate cancels (|v|/|w| < 1e-6): that step reduces the exact
+// norm before the JVP (its in-kernel scale), as does the last step.  When step j turns out to be
+// the last one, the JVP/multi-dot issued for j+1 are discarded (not counted).
+// NKHIP_LAGNORM=0 disables the lagged norm (every step reduces |v_{j+1}| first); so does a
+// problem that must not evaluate a discarded JVP (a user callback: scipy's exact F-call count).
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "nk_solver.h"
@@ -18,46 +29,36 @@ namespace nk {
 
 namespace {
 constexpr double kEps = DBL_EPSILON;
-}
+constexpr double kLagMinRatio2 = 1e-12;  // (|v|_est / |w|)^2 below which the estimate is not used
 
-int NewtonKrylov::issue_step(int j, int n_o, const double* sig, const double* rn, bool dev_scale) {
+bool lag_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("NKHIP_LAGNORM");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
+int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bool dev_scale) {
   const int64_t n = E_.n;
-  const double* z;
-  double zsig, zrn;
-  if (j < n_o) {  // augmentation vectors first (_gcrotmk.py:107-110)
-    const int slot = (ohead_ + j) % int(outer_.size());
-    z = outer_[slot];
-    zsig = osig_[slot];
-    zrn = orn_[slot];
-  } else if (j == n_o) {  // then v0 (:111-113)
-    z = V_[0];
-    zsig = sig[0];
-    zrn = rn[0];
-  } else {  // then the newest basis vector (:117-118)
-    z = V_[j];
-    zsig = dev_scale ? 0.0 : sig[j];
-    zrn = dev_scale ? 0.0 : rn[j];
-  }
   zp_[j] = z;
-  zs_[j] = zsig;  // fixed up by the caller once sig[j] is known (dev_scale)
+  zs_[j] = zs;  // provisional when the exact scale of z is only known later
   double* w = V_[j + 1];
   int rc;
-  if (dev_scale) {
+  if (dev_scale) {  // z = raw basis vector whose |z|^2 the combo left in device memory
     rc = P_.jvp_dev(X_, G0_, z, E_.dres(Engine::kSlotCombo), omega_, w);
     st_->njvp += 1;
-  } else {
-    const double nv = zsig * zrn;  // |z|_2 of the normalised vector (KrylovJacobian.matvec)
-    if (nv == 0.0) {
-      rc = E_.launch(K_COPY, 8.0 * n,
-                     [&] { return hipMemsetAsync(w, 0, sizeof(double) * n, E_.s); });
-    } else {
-      rc = P_.jvp(X_, G0_, z, zsig, omega_ / nv, w);
-      st_->njvp += 1;
-    }
+  } else if (znorm == 0.0) {  // KrylovJacobian.matvec: a zero vector maps to zero, no F call
+    rc = E_.launch(K_COPY, 8.0 * n,
+                   [&] { return hipMemsetAsync(w, 0, sizeof(double) * n, E_.s); });
+  } else {  // sc = omega / |v| with v = zs z (_nonlin.py:1505-1507)
+    rc = P_.jvp(X_, G0_, z, zs, omega_ / znorm, w);
+    st_->njvp += 1;
   }
   if (rc) return rc;
   st_->n_arnoldi += 1;
-  // one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i < j), |w|^2
+  // one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i <= j, the diagonal is |v_j|^2), |w|^2
   VecList P;
   for (int i = 0; i <= j; ++i) P.p[i] = V_[i];
   int64_t nblk = 0;
@@ -84,8 +85,10 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   const int n_o = ocount_;
   const int m = o_.inner_m + n_o;
   const int64_t n = E_.n;
+  const int K = int(outer_.size());
+  const bool lag = lag_enabled() && P_.may_speculate();
   V_[0] = Fx_;  // v0 = b / |b|, kept raw with scale 1/|b|
-  double sig[kMaxVec + 2], rn[kMaxVec + 2];
+  double sig[kMaxVec + 2], rn[kMaxVec + 2], sig_est[kMaxVec + 2], wnorm[kMaxVec + 2];
   sig[0] = 1.0 / b_norm;
   rn[0] = b_norm;
   static thread_local double R[kMaxVec + 1][kMaxVec + 1];
@@ -94,82 +97,159 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   double red[2 * kMaxVec + 2];
   for (int i = 0; i < kMaxVec + 2; ++i) gv[i] = 0.0;
   gv[0] = 1.0;
-  int j = 0;
-  bool breakdown = false;
-  bool pending = false;  // a speculative JVP/multi-dot for step j+1 is in flight
-  int rc = issue_step(0, n_o, sig, rn, false);
+
+  // input of step j whose scale is known on the host: the augmentation vectors first
+  // (_gcrotmk.py:107-110), then v0 (:111-113), then the newest basis vector (:117-118)
+  auto input = [&](int j, const double** z, double* zs, double* zn) {
+    if (j < n_o) {
+      const int slot = (ohead_ + j) % K;
+      *z = outer_[slot];
+      *zs = osig_[slot];
+      *zn = osig_[slot] * orn_[slot];
+    } else {
+      *z = V_[j > n_o ? j : 0];
+      const int q = j > n_o ? j : 0;
+      *zs = sig[q];
+      *zn = sig[q] * rn[q];
+    }
+  };
+  // Step i is complete once hn = |v_{i+1}| (raw) is known: Hessenberg column i, Givens update of
+  // its QR (qr_insert, _gcrotmk.py:146-158), residual test (:165).  True when the process stops.
+  auto finish = [&](int i, double hn) -> bool {
+    for (int k = 0; k <= i; ++k) hcur[k] = h[k];
+    hcur[i + 1] = hn;
+    const double alpha = 1.0 / hn;
+    sig[i + 1] = std::isfinite(alpha) ? alpha : 1.0;  // scipy leaves w unscaled then
+    rn[i + 1] = hn;
+    const bool breakdown = !(hn > kEps * wnorm[i]);
+    for (int k = 0; k < i; ++k) {
+      const double t = cs[k] * hcur[k] + sn[k] * hcur[k + 1];
+      hcur[k + 1] = -sn[k] * hcur[k] + cs[k] * hcur[k + 1];
+      hcur[k] = t;
+    }
+    detail::givens(hcur[i], hcur[i + 1], &cs[i], &sn[i]);
+    hcur[i] = cs[i] * hcur[i] + sn[i] * hcur[i + 1];
+    for (int k = 0; k <= i; ++k) R[k][i] = hcur[k];
+    gv[i + 1] = -sn[i] * gv[i];
+    gv[i] = cs[i] * gv[i];
+    return std::fabs(gv[i + 1]) < ptol || breakdown;
+  };
+
+  int rc;
+  {
+    const double* z;
+    double zs, zn;
+    input(0, &z, &zs, &zn);
+    rc = issue_step(0, z, zs, zn, false);
+  }
+  sig_est[0] = 0.0;
   if (!rc) rc = E_.sync();
   if (rc) return rc;
-  for (j = 0; j < m; ++j) {
+  int j = 0, last = 0;
+  bool hn_pending = false;  // step j-1 still waits for |v_j| (Gram diagonal of multi-dot j)
+  for (;;) {
     // -- results of the multi-dot of step j
     const int np = j + 1;
     std::memcpy(red, E_.hres(Engine::kSlotMdot), sizeof(double) * (2 * np + 1));
-    const double ww = red[2 * np];
+    double tau = 1.0;
+    if (hn_pending) {
+      hn_pending = false;
+      if (finish(j - 1, std::sqrt(red[np + j]))) {  // step j's JVP/multi-dot are not part of it
+        st_->njvp -= 1;
+        st_->n_arnoldi -= 1;
+        last = j - 1;
+        break;
+      }
+      if (sig_est[j] > 0.0) {  // JVP_j saw v_j scaled by sig_est instead of the exact sig
+        tau = sig[j] / sig_est[j];
+        zs_[j] = sig[j];
+      }
+    }
+    const double ww = tau * tau * red[2 * np];
     if (!std::isfinite(ww)) return NK_NONFINITE;  // _nonlin.py:1511-1512
-    const double w_norm = std::sqrt(ww);
+    wnorm[j] = std::sqrt(ww);
     for (int i = 0; i < j; ++i) gram[j][i] = sig[j] * sig[i] * red[np + i];
     // MGS coefficients from the Gram matrix: (I + L) h = V^T w (inverse compact WY form)
+    double hh = 0.0;
     for (int i = 0; i <= j; ++i) {
-      double acc = sig[i] * red[i];
+      double acc = tau * sig[i] * red[i];
       for (int k = 0; k < i; ++k) acc -= gram[i][k] * h[k];
       h[i] = acc;
+      hh += acc * acc;
     }
-    // -- v_{j+1} = w - V h and |v_{j+1}|^2 in one pass
     VecList U;
     for (int i = 0; i <= j; ++i) {
       U.p[i] = V_[i];
       U.c[i] = -h[i] * sig[i];
     }
     double* w = V_[j + 1];
+    const bool more = j + 1 < m;
+    const bool next_is_v = more && (j + 1 > n_o);  // step j+1 applies J to v_{j+1} itself
+    const double est = ww - hh;                    // |v_{j+1}|^2 = |w|^2 - |h|^2
+    const bool lag_step = more && lag && (!next_is_v || est > kLagMinRatio2 * ww);
     int64_t nblk = 0;
+    if (lag_step) {
+      // -- v_{j+1} = tau w - V h (no reduction), then step j+1 right away
+      rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
+        return combo_launch(w, w, tau, U, j + 1, n, nullptr, E_.s, &nblk);
+      });
+      if (rc) return rc;
+      const double* z;
+      double zs, zn;
+      if (next_is_v) {
+        const double e = std::sqrt(est);
+        z = w;
+        zs = 1.0 / e;
+        zn = zs * e;
+        sig_est[j + 1] = zs;
+      } else {
+        input(j + 1, &z, &zs, &zn);
+        sig_est[j + 1] = 0.0;
+      }
+      rc = issue_step(j + 1, z, zs, zn, false);
+      if (!rc) rc = E_.sync();
+      if (rc) return rc;
+      hn_pending = true;
+      ++j;
+      continue;
+    }
+    // -- v_{j+1} = tau w - V h and its exact |v_{j+1}|^2 before the next JVP
     rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
-      return combo_launch(w, w, 1.0, U, j + 1, n, E_.partial(), E_.s, &nblk);
+      return combo_launch(w, w, tau, U, j + 1, n, E_.partial(), E_.s, &nblk);
     });
     // only |v_{j+1}|^2 is used (a non-finite v shows up in it): one sum, one all-reduce on N GPUs
     if (!rc) rc = E_.reduce_async(nblk, 1, 1, Engine::kSlotCombo);
     if (rc) return rc;
-    // -- speculatively start step j+1 when its direction is v_{j+1} (device-side JVP scale)
-    const bool more = j + 1 < m;
-    pending = more && (j + 1 > n_o) && P_.has_dev_scale();
-    if (pending) {
-      rc = issue_step(j + 1, n_o, sig, rn, true);
+    // speculatively start step j+1 with its scale taken from the device norm
+    const bool spec = next_is_v && P_.has_dev_scale() && P_.may_speculate();
+    if (spec) {
+      rc = issue_step(j + 1, w, 0.0, 0.0, true);
       if (rc) return rc;
     }
     rc = E_.sync();
     if (rc) return rc;
-    const double hn = std::sqrt(E_.hres(Engine::kSlotCombo)[0]);
-    for (int i = 0; i <= j; ++i) hcur[i] = h[i];
-    hcur[j + 1] = hn;
-    const double alpha = 1.0 / hn;
-    sig[j + 1] = std::isfinite(alpha) ? alpha : 1.0;  // scipy leaves w unscaled then
-    rn[j + 1] = hn;
-    if (pending) zs_[j + 1] = sig[j + 1];
-    if (!(hn > kEps * w_norm)) breakdown = true;
-    // -- Givens update of the Hessenberg QR (qr_insert, _gcrotmk.py:146-158)
-    for (int i = 0; i < j; ++i) {
-      const double t = cs[i] * hcur[i] + sn[i] * hcur[i + 1];
-      hcur[i + 1] = -sn[i] * hcur[i] + cs[i] * hcur[i + 1];
-      hcur[i] = t;
+    const bool stop = finish(j, std::sqrt(E_.hres(Engine::kSlotCombo)[0]));
+    if (spec) zs_[j + 1] = sig[j + 1];
+    if (stop || !more) {
+      if (spec) {  // the step issued for j+1 is not part of the Arnoldi process
+        st_->njvp -= 1;
+        st_->n_arnoldi -= 1;
+      }
+      last = j;
+      break;
     }
-    detail::givens(hcur[j], hcur[j + 1], &cs[j], &sn[j]);
-    hcur[j] = cs[j] * hcur[j] + sn[j] * hcur[j + 1];
-    for (int i = 0; i <= j; ++i) R[i][j] = hcur[i];
-    gv[j + 1] = -sn[j] * gv[j];
-    gv[j] = cs[j] * gv[j];
-    const double res = std::fabs(gv[j + 1]);
-    if (res < ptol || breakdown) break;
-    if (more && !pending) {
-      rc = issue_step(j + 1, n_o, sig, rn, false);
+    if (!spec) {
+      const double* z;
+      double zs, zn;
+      input(j + 1, &z, &zs, &zn);
+      rc = issue_step(j + 1, z, zs, zn, false);
       if (!rc) rc = E_.sync();
       if (rc) return rc;
     }
-    pending = false;
+    sig_est[j + 1] = 0.0;
+    ++j;
   }
-  if (pending) {  // the step issued for j+1 is not part of the Arnoldi process
-    st_->njvp -= 1;
-    st_->n_arnoldi -= 1;
-  }
-  if (j == m) j = m - 1;
+  j = last;
   if (!std::isfinite(R[j][j])) return NK_OK;  // LinAlgError -> lgmres returns x = 0
   double y[kMaxVec + 1];
   detail::lstsq_upper(R, j + 1, gv, y);
@@ -179,7 +259,6 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   }
   // -- dx = sum_i y_i z_i into the next outer slot (the oldest one if the ring is full; the
   //    combination reads each element before writing it, so in-place is safe)
-  const int K = int(outer_.size());
   const int slot = (o_.outer_k > 0 && ocount_ < o_.outer_k) ? (ohead_ + ocount_) % K : ohead_;
   VecList Z;
   for (int i = 0; i <= j; ++i) {

@@ -5,9 +5,11 @@
 // main.cpp:104), re-designed for one GPU stream per rank:
 //   * every N^2-sized vector lives in HBM; the host only holds scalars and the <= 64x64
 //     Hessenberg factorisation;
-//   * per Arnoldi step: one JVP kernel, one fused multi-dot (V^T w, new Gram row, |w|^2),
-//     one fused update (w - V h, |w'|^2) -- the MGS coefficients are recovered from the Gram
-//     row (inverse compact-WY MGS), which equals scipy's MGS in exact arithmetic;
+//   * per Arnoldi step: one JVP kernel, one fused multi-dot (V^T w, new Gram row incl. the
+//     previous vector's |v|^2, |w|^2), one update (w - V h) -- the MGS coefficients are recovered
+//     from the Gram row (inverse compact-WY MGS), which equals scipy's MGS in exact arithmetic;
+//     the norm of the new vector arrives with the next multi-dot (lgmres.cpp), so a step costs
+//     one reduction and one host synchronisation;
 //   * basis vectors are kept un-normalised with a host-side scale (no scal pass).
 #pragma once
 
@@ -146,6 +148,9 @@ struct Problem {
                       const double* /*znorm2*/, double /*omega*/, double* /*w*/) {
     return NK_EINVAL;
   }
+  // May the solver evaluate a JVP it later discards (the step after the last Arnoldi step)?  A
+  // user callback must see exactly scipy's F calls, so the generic problem says no.
+  virtual bool may_speculate() const { return true; }
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
 };
@@ -164,7 +169,7 @@ class NewtonKrylov {
  private:
   int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
   // Launch JVP_j (w = V[j+1] = J z_j) and the fused multi-dot of step j; no synchronisation.
-  int issue_step(int j, int n_o, const double* sig, const double* rn, bool dev_scale);
+  int issue_step(int j, const double* z, double zs, double znorm, bool dev_scale);
   const double* zp_[kMaxVec + 1];
   double zs_[kMaxVec + 1];
   int line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax);

@@ -58,6 +58,7 @@ class CallbackProblem final : public Problem {
            double red[3]) override;
   int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
           double* w) override;
+  bool may_speculate() const override { return false; }  // scipy calls F exactly nfev + njvp times
 
  private:
   int norms(double* v, double* sum2, double* vmax);

@@ -18,6 +18,9 @@ container's SciPy 1.15.3 is the de-facto pin.  This file restates its published 
 ``ortho="icwy"`` swaps MGS for the inverse-compact-WY form of MGS (one fused multi-dot + one
 update per Arnoldi step) that the HIP solver uses; it is equal to MGS in exact arithmetic and
 exists here only so that the CPU tests can show the two agree on the SH problem.
+``ortho="lag"`` is icwy with the HIP solver's lagged norm (csrc/lgmres.cpp): the JVP of a new
+basis vector is applied to ``v_raw / sqrt(|w|^2 - |h|^2)`` (norm 1 up to rounding, the FD step
+taken as ``omega``) and rescaled once the exact norm is known.
 """
 from __future__ import annotations
 
@@ -90,6 +93,8 @@ def fgmres(matvec, v0, m, atol, outer_v, stats, ortho="mgs"):
     breakdown = False
     res = math.nan
     j = 0
+    est = -1.0  # lag: |w|^2 - |h|^2 of the previous step
+    wraw = None
     for j in range(m):
         if j < n_outer:
             z = outer_v[j]
@@ -97,7 +102,11 @@ def fgmres(matvec, v0, m, atol, outer_v, stats, ortho="mgs"):
             z = v0
         else:
             z = vs[-1]
-        w = matvec(z)
+        if ortho == "lag" and j > n_outer and est > 1e-12 * wwprev:
+            e = math.sqrt(est)
+            w = (e / hprev) * matvec(wraw / e, unit=True)
+        else:
+            w = matvec(z)
         stats.arnoldi += 1
         w_norm = _norm(w)
         hcur = np.zeros(j + 2)
@@ -115,7 +124,11 @@ def fgmres(matvec, v0, m, atol, outer_v, stats, ortho="mgs"):
                 h[i] = c[i] - gram[i, :i] @ h[:i]
             hcur[:j + 1] = h
             w = w - sum(h[i] * vs[i] for i in range(j + 1))
+            wwprev = w_norm * w_norm
+            est = wwprev - float(h @ h)
+            wraw = w
         hcur[j + 1] = _norm(w)
+        hprev = hcur[j + 1]
         with np.errstate(over="ignore", divide="ignore"):
             alpha = 1.0 / hcur[-1]
         if np.isfinite(alpha):
@@ -163,8 +176,8 @@ class KrylovJacobian:
         self.f0 = f
         self.omega = self.rdiff * max(1.0, maxnorm(x)) / max(1.0, maxnorm(f))
 
-    def matvec(self, v):
-        nv = _norm(v)
+    def matvec(self, v, unit=False):
+        nv = 1.0 if unit else _norm(v)
         if nv == 0:
             return 0 * v
         sc = self.omega / nv

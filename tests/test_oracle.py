@@ -58,7 +58,7 @@ NK = ["nk_n61_default", "nk_n61_tight", "nk_n64_default", "nk_n64_h0625_tight",
 
 
 @pytest.mark.parametrize("name", NK)
-@pytest.mark.parametrize("ortho", ["mgs", "icwy"])
+@pytest.mark.parametrize("ortho", ["mgs", "icwy", "lag"])
 def test_nk_restatement_matches_scipy_steps(name, ortho):
     z = load_golden(name)
     N, h, r, k, g = int(z["N"]), float(z["h"]), float(z["r"]), float(z["k"]), float(z["g"])
