@@ -101,6 +101,14 @@ int nk_sh_residual(const double* u_dev, const double* uo_dev, double* F_dev, int
 int nk_sh_jvp(const double* u_dev, const double* v_dev, double* y_dev, int64_t ny, int64_t nx,
               double h, double r, double k, double g, void* stream);
 
+/* y = (G(x0 + sc*zs*z) - G0) / sc, the finite-difference matvec of KrylovJacobian
+ * (scipy/optimize/_nonlin.py:1500-1513) with the solver's split F(u) = G(u) + B(uo):
+ * G(w) = w/k - (L w + g w^2 - w^3)/2 and G0 = G(x0) (pass y = F(x0+..) - F(x0) over sc when G0 is
+ * F(x0) - B).  One fused pass reading x0, z, G0: the kernel inside every Arnoldi step. */
+int nk_sh_fdjvp(const double* x0_dev, const double* G0_dev, const double* z_dev, double* y_dev,
+                int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
+                double sc, void* stream);
+
 /* ---------------- BLAS-1 (scipy get_blas_funcs dot/nrm2/axpy/scal in _gcrotmk.py:104-126) ------ */
 /* Scalar results are written to host memory; the call synchronises `stream`. */
 int nk_dot(const double* x_dev, const double* y_dev, int64_t n, double* out, void* stream);

@@ -134,6 +134,23 @@ int nk_sh_jvp(const double* u, const double* v, double* y, int64_t ny, int64_t n
   return hip_rc(stencil_launch(SMode::AJVP, A, S(stream), nullptr));
 }
 
+int nk_sh_fdjvp(const double* x0, const double* G0, const double* z, double* y, int64_t ny,
+                int64_t nx, double h, double r, double k, double g, double zs, double sc,
+                void* stream) {
+  if (!x0 || !G0 || !z || !y || ny <= 0 || nx <= 0 || !(sc != 0.0)) return NK_EINVAL;
+  StencilArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.a = periodic(x0);
+  A.b = periodic(z);
+  A.alpha = sc * zs;
+  A.sc = sc;
+  A.p0 = G0;
+  A.out0 = y;
+  A.c = sh_coef(h, r, k, g);
+  return hip_rc(stencil_launch(SMode::FDJVP, A, S(stream), nullptr));
+}
+
 // ------------------------------------------------------------------------------ BLAS-1
 int nk_dot(const double* x, const double* y, int64_t n, double* out, void* stream) {
   if (!x || !y || !out || n < 0) return NK_EINVAL;

@@ -153,11 +153,22 @@ __device__ __forceinline__ double2 ld_p0(const StencilArgs& A, const double* p) 
 // ------------------------------------------------------------------------------------------
 // march kernel
 // ------------------------------------------------------------------------------------------
-template <SMode M, int BX>
+// A band of rows is walked with a ring of RING = NR + PF row slots: NR rows form the stencil
+// window, PF more are in flight.  The walk is unrolled by RING, so the window "shift" is a
+// compile-time renaming of ring slots, not a register copy: a copy would need the freshly loaded
+// row to have arrived, and the in-order vmcnt would then drain every load at the end of each
+// row (the previous design's limit: one row of loads in flight per wave).  Here the compute of
+// row r waits only for the loads issued PF rows earlier.  Raw rows are kept per field; the FD
+// combination a + alpha*b is formed when a row is first used, not when it is loaded.
+template <SMode M>
+constexpr int kFields = (kComb<M> || kTwo<M>) ? 2 : 1;
+
+template <SMode M, int BX, int PF>
 __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   constexpr int R = kRad<M>;
   constexpr int NR = 2 * R + 1;
-  constexpr int NB = kTwo<M> ? NR : 1;
+  constexpr int RING = NR + PF;
+  constexpr int NF = kFields<M>;
   const int64_t nx = A.nx, ny = A.ny;
   const int64_t c0 = 2 * (int64_t(blockIdx.x) * BX + threadIdx.x);
   const bool active = c0 < nx;
@@ -174,23 +185,28 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
     const double2 x2 = *reinterpret_cast<const double2*>(p + cp);
     v[0] = x0.x; v[1] = x0.y; v[2] = x1.x; v[3] = x1.y; v[4] = x2.x; v[5] = x2.y;
   };
-  auto ldw = [&](int64_t r, double (&va)[6], double (&vb)[6]) {
-    ld(A.a, r, va);
+  // ring[f][slot][6]: raw rows of field f (a, then b)
+  double ring[NF][RING][6];
+  auto load_row = [&](int slot, int64_t r) {
+    r = (r > ny + 1) ? ny + 1 : ((r < -2) ? -2 : r);  // past the band: a valid halo / edge row
+    ld(A.a, r, ring[0][slot]);
+    if constexpr (NF == 2) ld(A.b, r, ring[1][slot]);
+  };
+  // a + alpha b, formed once when the row enters the window
+  auto combine = [&](int slot) {
     if constexpr (kComb<M>) {
-      double t[6];
-      ld(A.b, r, t);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) va[q] = va[q] + alpha * t[q];
-    } else if constexpr (kTwo<M>) {
-      ld(A.b, r, vb);
+      for (int q = 0; q < 6; ++q) ring[0][slot][q] = ring[0][slot][q] + alpha * ring[1][slot][q];
     }
   };
+  auto ldp = [&](int64_t r) {
+    r = (r >= ny) ? ny - 1 : ((r < 0) ? 0 : r);
+    return ld_p0(A, A.p0 + r * nx + cc);
+  };
 
-  double wa[NR][6], wb[NB][6];
-  double na_[6], nb_[6];
   // Odd bands march upwards: a band boundary is then reached by both adjacent bands at the same
   // time (both at their start or both at their end), so the halo rows one band re-reads are still
-  // in L2.  The window sums below pair the rows symmetrically about the centre, so the result is
+  // in L2.  The window sums pair the rows symmetrically about the centre, so the result is
   // bitwise the same in either direction (fp addition is commutative).
   // A.rev walks the bands from the top of the grid (see traversal_reverse)
   const int64_t band = A.rev ? int64_t(gridDim.y) - 1 - blockIdx.y : int64_t(blockIdx.y);
@@ -199,81 +215,74 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   const bool up = (band & 1) != 0;
   const int64_t dir = up ? -1 : 1;
   const int64_t rs = up ? r1 - 1 : r0;
+  const int64_t nrows = r1 - r0;
+
+  // prologue: slot k holds row rs + dir*(k - R) (window rows and PF - 1 rows in flight)
 #pragma unroll
-  for (int m = 0; m < NR; ++m) ldw(rs + dir * (m - R), wa[m], wb[kTwo<M> ? m : 0]);
+  for (int k = 0; k < RING - 1; ++k) load_row(k, rs + dir * (k - R));
+  double2 pq[RING];
+#pragma unroll
+  for (int d = 0; d < RING; ++d) pq[d] = make_double2(0.0, 0.0);
+  if constexpr (kHasP0<M>) {
+#pragma unroll
+    for (int d = 0; d < PF; ++d) pq[d] = ldp(rs + dir * d);
+  }
+#pragma unroll
+  for (int k = 0; k < NR - 1; ++k) combine(k);
 
   double red[3] = {0.0, 0.0, 0.0};
-  // the point-wise input is prefetched one row ahead as well, so that the compute of row r waits
-  // only for loads issued during the previous iteration (in-order vmcnt)
-  double2 pv_next = make_double2(0.0, 0.0);
-  if constexpr (kHasP0<M>) pv_next = ld_p0(A, A.p0 + rs * nx + cc);
-  for (int64_t it = 0; it < r1 - r0; ++it) {
-    const int64_t r = rs + dir * it;
-    const int64_t o = r * nx + cc;
-    const double2 pv = pv_next;
-    if constexpr (kHasP0<M>) {
-      int64_t rp = r + dir;
-      rp = (rp >= ny) ? ny - 1 : ((rp < 0) ? 0 : rp);
-      pv_next = ld_p0(A, A.p0 + rp * nx + cc);
-    }
-    // prefetch the next entering row (unconditionally: past the band end it re-reads a valid
-    // halo row, which keeps the load count per iteration fixed for the waitcnt schedule)
-    int64_t rn = r + dir * (R + 1);
-    rn = (rn > ny + 1) ? ny + 1 : ((rn < -2) ? -2 : rn);
-    ldw(rn, na_, nb_);
-    Res res[2];
+  for (int64_t base = 0; base < nrows; base += RING) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      Nb a, b{0.0, 0.0, 0.0, 0.0};
-      if constexpr (R == 2) {
-        a.c = wa[2][2 + q];
-        a.a1 = (wa[2][1 + q] + wa[2][3 + q]) + (wa[1][2 + q] + wa[3][2 + q]);
-        a.dg = (wa[1][1 + q] + wa[1][3 + q]) + (wa[3][1 + q] + wa[3][3 + q]);
-        a.a2 = (wa[2][q] + wa[2][4 + q]) + (wa[0][2 + q] + wa[4][2 + q]);
-        if constexpr (kTwo<M>) {
-          b.c = wb[2][2 + q];
-          b.a1 = (wb[2][1 + q] + wb[2][3 + q]) + (wb[1][2 + q] + wb[3][2 + q]);
-          b.dg = (wb[1][1 + q] + wb[1][3 + q]) + (wb[3][1 + q] + wb[3][3 + q]);
-          b.a2 = (wb[2][q] + wb[2][4 + q]) + (wb[0][2 + q] + wb[4][2 + q]);
+    for (int u = 0; u < RING; ++u) {
+      const int64_t it = base + u;  // rows past the band end are computed but not stored
+      const int64_t r = rs + dir * it;
+      load_row((u + RING - 1) % RING, r + dir * (R + PF));
+      if constexpr (kHasP0<M>) pq[(u + PF) % RING] = ldp(r + dir * PF);
+      combine((u + NR - 1) % RING);
+      const double2 pv = pq[u % RING];
+      auto W = [&](int m, int q) -> double { return ring[0][(u + m) % RING][q]; };
+      auto Wb = [&](int m, int q) -> double { return ring[NF - 1][(u + m) % RING][q]; };
+      Res res[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        Nb na, nb{0.0, 0.0, 0.0, 0.0};
+        if constexpr (R == 2) {
+          na.c = W(2, 2 + q);
+          na.a1 = (W(2, 1 + q) + W(2, 3 + q)) + (W(1, 2 + q) + W(3, 2 + q));
+          na.dg = (W(1, 1 + q) + W(1, 3 + q)) + (W(3, 1 + q) + W(3, 3 + q));
+          na.a2 = (W(2, q) + W(2, 4 + q)) + (W(0, 2 + q) + W(4, 2 + q));
+          if constexpr (kTwo<M>) {
+            nb.c = Wb(2, 2 + q);
+            nb.a1 = (Wb(2, 1 + q) + Wb(2, 3 + q)) + (Wb(1, 2 + q) + Wb(3, 2 + q));
+            nb.dg = (Wb(1, 1 + q) + Wb(1, 3 + q)) + (Wb(3, 1 + q) + Wb(3, 3 + q));
+            nb.a2 = (Wb(2, q) + Wb(2, 4 + q)) + (Wb(0, 2 + q) + Wb(4, 2 + q));
+          }
+        } else {
+          na.c = W(1, 2 + q);
+          na.a1 = (W(1, 1 + q) + W(1, 3 + q)) + (W(0, 2 + q) + W(2, 2 + q));
+          na.dg = 0.0;
+          na.a2 = 0.0;
         }
-      } else {
-        a.c = wa[1][2 + q];
-        a.a1 = (wa[1][1 + q] + wa[1][3 + q]) + (wa[0][2 + q] + wa[2][2 + q]);
-        a.dg = 0.0;
-        a.a2 = 0.0;
+        res[q] = finish<M>(A, na, nb, q == 0 ? pv.x : pv.y, alpha, sc);
       }
-      res[q] = finish<M>(A, a, b, q == 0 ? pv.x : pv.y, alpha, sc);
-    }
-    if (active) {
-      *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
-      if constexpr (M == SMode::TRIAL) {
-        *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
-        if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+      if (active && it < nrows) {
+        const int64_t o = r * nx + cc;
+        *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
+        if constexpr (M == SMode::TRIAL) {
+          *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
+          if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          red[0] += res[q].o0 * res[q].o0;
-          red[1] = nmax(red[1], fabs(res[q].o0));
-          red[2] = nmax(red[2], fabs(res[q].o2));
+          for (int q = 0; q < 2; ++q) {
+            red[0] += res[q].o0 * res[q].o0;
+            red[1] = nmax(red[1], fabs(res[q].o0));
+            red[2] = nmax(red[2], fabs(res[q].o2));
+          }
+        } else if constexpr (M == SMode::LINOP) {
+          *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) red[0] += res[q].o2 * res[q].o0;
         }
-      } else if constexpr (M == SMode::LINOP) {
-        *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) red[0] += res[q].o2 * res[q].o0;
       }
-    }
-    // shift the window up by one row
-#pragma unroll
-    for (int m = 0; m < NR - 1; ++m) {
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        wa[m][q] = wa[m + 1][q];
-        if constexpr (kTwo<M>) wb[m][q] = wb[m + 1][q];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      wa[NR - 1][q] = na_[q];
-      if constexpr (kTwo<M>) wb[NR - 1][q] = nb_[q];
     }
   }
   if constexpr (kRed<M>) {
@@ -372,25 +381,30 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
         f->hi = f->base;
       }
     }
-    // Row band per block: aim for >= ~4096 blocks (16 per CU) with bands of 4..32 rows
-    // (4096^2: RY = 16, measured best of 8..256).
-    // (NKHIP_RY_MIN / NKHIP_RY_MAX / NKHIP_BLOCKS override the choice for tuning runs.)
-    static const int ry_min = env_int("NKHIP_RY_MIN", 4);
-    static const int ry_max = env_int("NKHIP_RY_MAX", 32);
+    // Row band per block: a multiple of the ring length RING (the unroll of the walk), aiming at
+    // >= ~4096 blocks (16 per CU) for the grid (NKHIP_BLOCKS / NKHIP_PF override for tuning).
     static const int blocks = env_int("NKHIP_BLOCKS", 4096);
+    static const int pf = env_int("NKHIP_PF", 1);
     constexpr int BX = 128;
+    constexpr int R = kRad<M>;
+    const int ring = 2 * R + 1 + (pf == 2 ? 2 : 1);
     const int64_t gx = (A.nx / 2 + BX - 1) / BX;
-    int64_t ry = (A.ny * gx) / blocks;
-    int RY = ry_min;
-    while (RY < ry_max && RY * 2 <= ry) RY *= 2;
+    const int64_t want = (A.ny * gx) / blocks;  // rows per band for `blocks` blocks
+    int64_t k = (want + ring / 2) / ring;
+    if (k < 1) k = 1;
+    if (k > 6) k = 6;
+    const int RY = int(k * ring);
     const int64_t gy = (A.ny + RY - 1) / RY;
     if (gy > 65535) return hipErrorInvalidValue;
     if (nblk) *nblk = gx * gy;
     B.rev = traversal_reverse();
     static const bool nt_p0 = env_int("NKHIP_NT_P0", 1) != 0;
     B.nt_p0 = nt_p0;
-    hipLaunchKernelGGL((march_kernel<M, BX>), dim3(unsigned(gx), unsigned(gy)), dim3(BX), 0, s, B,
-                       RY);
+    const dim3 grid{unsigned(gx), unsigned(gy), 1u};
+    if (pf == 2)
+      hipLaunchKernelGGL((march_kernel<M, BX, 2>), grid, dim3(BX), 0, s, B, RY);
+    else
+      hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY);
   } else {
     const int64_t n = A.nx * A.ny;
     const int64_t g = (n + 255) / 256;
@@ -418,7 +432,7 @@ hipError_t stencil_launch(SMode m, const StencilArgs& a, hipStream_t s, int64_t*
 }
 
 int64_t stencil_partial_slots(int64_t ny, int64_t nx) {
-  const int64_t march = ((nx / 2 + 127) / 128) * ((ny + 3) / 4);  // RY >= 4, BX = 128
+  const int64_t march = ((nx / 2 + 127) / 128) * ((ny + 3) / 4);  // RY >= 4 (a ring), BX = 128
   const int64_t point = (nx * ny + 255) / 256;
   return 3 * (march > point ? march : point) + 3;
 }

@@ -76,6 +76,7 @@ SIGNATURES = [
     ("nk_sh13_apply", C.c_int, [_P, _P, _I64, _I64, _D, _D, _P]),
     ("nk_sh_residual", C.c_int, [_P, _P, _P, _I64, _I64, _D, _D, _D, _D, _P]),
     ("nk_sh_jvp", C.c_int, [_P, _P, _P, _I64, _I64, _D, _D, _D, _D, _P]),
+    ("nk_sh_fdjvp", C.c_int, [_P, _P, _P, _P, _I64, _I64, _D, _D, _D, _D, _D, _D, _P]),
     ("nk_dot", C.c_int, [_P, _P, _I64, C.POINTER(_D), _P]),
     ("nk_nrm2", C.c_int, [_P, _I64, C.POINTER(_D), _P]),
     ("nk_maxnorm", C.c_int, [_P, _I64, C.POINTER(_D), _P]),

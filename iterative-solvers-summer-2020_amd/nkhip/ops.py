@@ -84,6 +84,18 @@ def sh_jvp(u, v, h, r, k, g, ny=None, nx=None, out=None):
     return out
 
 
+def sh_fdjvp(x0, G0, z, h, r, k, g, zs, sc, ny=None, nx=None, out=None):
+    """FD matvec of KrylovJacobian (_nonlin.py:1500-1513): (G(x0 + sc*zs*z) - G0)/sc with
+    G(w) = w/k - (L w + g w^2 - w^3)/2 (the x-dependent part of the residual)."""
+    for t, nm in ((x0, "x0"), (G0, "G0"), (z, "z")):
+        _dev(t, nm)
+    ny, nx = _grid(x0, ny, nx)
+    out = torch.empty_like(x0) if out is None else _dev(out, "out")
+    check(lib.nk_sh_fdjvp(_ptr(x0), _ptr(G0), _ptr(z), _ptr(out), ny, nx, float(h), float(r),
+                          float(k), float(g), float(zs), float(sc), _stream()), "nk_sh_fdjvp")
+    return out
+
+
 def dot(x, y) -> float:
     _dev(x, "x")
     _dev(y, "y")

@@ -67,6 +67,31 @@ def test_residual_and_jvp_vs_oracle(N):
     assert _rel(J, sh_oracle.jvp(u, v, N, N, h, r, k, g)) <= 1e-12
 
 
+@pytest.mark.parametrize("N", [61, 64, 256])
+def test_fd_matvec_vs_oracle(N):
+    """nk_sh_fdjvp = KrylovJacobian.matvec's (F(x0 + sc v) - F(x0))/sc (_nonlin.py:1505-1509) on the
+    x-dependent part G of the residual.  A difference quotient amplifies the rounding of G by 1/sc
+    (with scipy's own step, omega = sqrt(eps)|x0|/|F0| ~ 1e-10 here, that noise is ~1e-4 of the
+    result), so the kernel arithmetic is checked at a step where the noise is ~1e-9: against the
+    oracle's quotient to 1e-7 relative, and against the analytic J v to the O(sc) truncation."""
+    import nkhip
+    rng = np.random.default_rng(N + 1)
+    x0, z = rng.standard_normal(N * N), rng.standard_normal(N * N)
+    h, r, k, g = 0.625, 0.01, 0.2, 1.0
+
+    def G(w):
+        return w / k - (sh_oracle.sh13(w, N, N, h, r) + g * w * w - w * w * w) / 2
+
+    G0 = G(x0)
+    zs = 1.0 / np.linalg.norm(z)
+    sc = 1e-4
+    y = nkhip.sh_fdjvp(_t(x0), _t(G0), _t(z), h, r, k, g, zs, sc, N, N)
+    ref = (G(x0 + sc * zs * z) - G0) / sc
+    assert _rel(y, ref) <= 1e-7
+    # and it is the Jacobian product up to the FD truncation error O(sc)
+    assert _rel(y, sh_oracle.jvp(x0, zs * z, N, N, h, r, k, g)) <= 1e-5
+
+
 @pytest.mark.parametrize("n", [1, 7, 2047, 2048, 2049, 100_001, 1 << 20])
 def test_blas1_vs_torch(n):
     import nkhip
