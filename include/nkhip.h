@@ -109,6 +109,19 @@ int nk_sh_fdjvp(const double* x0_dev, const double* G0_dev, const double* z_dev,
                 int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
                 double sc, void* stream);
 
+/* One fused Arnoldi step of the solver (the loop body of scipy's _fgmres between two matvecs,
+ * scipy/sparse/linalg/_isolve/_gcrotmk.py:104-143, plus the next KrylovJacobian.matvec,
+ * scipy/optimize/_nonlin.py:1500-1513), in one pass over the basis:
+ *   v = tau*w + sum_i coef[i]*V[i]                 -> v_out
+ *   w' = (G(x0 + sc*zs*z) - G0)/sc,  z = v if z_dev == NULL   -> w_out
+ *   dots[0..2nv+2] = [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']  (host; NULL: no reduction,
+ *   no synchronisation).  nv <= 32, ny, nx >= 8, periodic grid; v_out must not alias w or V[i]. */
+int nk_sh_arnoldi_fused(const double* const* V_dev, const double* coef, int32_t nv,
+                        const double* w_dev, double tau, const double* x0_dev, const double* G0_dev,
+                        const double* z_dev, int64_t ny, int64_t nx, double h, double r, double k,
+                        double g, double zs, double sc, double* v_out_dev, double* w_out_dev,
+                        double* dots, void* stream);
+
 /* ---------------- BLAS-1 (scipy get_blas_funcs dot/nrm2/axpy/scal in _gcrotmk.py:104-126) ------ */
 /* Scalar results are written to host memory; the call synchronises `stream`. */
 int nk_dot(const double* x_dev, const double* y_dev, int64_t n, double* out, void* stream);

@@ -151,6 +151,57 @@ int nk_sh_fdjvp(const double* x0, const double* G0, const double* z, double* y, 
   return hip_rc(stencil_launch(SMode::FDJVP, A, S(stream), nullptr));
 }
 
+int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, const double* w,
+                        double tau, const double* x0, const double* G0, const double* z,
+                        int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
+                        double sc, double* v_out, double* w_out, double* dots, void* stream) {
+  if (!V || !coef || !w || !x0 || !G0 || !v_out || !w_out || !(sc != 0.0)) return NK_EINVAL;
+  if (!arnoldi_supported(nv, ny, nx)) return NK_EINVAL;
+  ArnoldiArgs A;
+  A.ny = ny;
+  A.nx = nx;
+  A.nv = nv;
+  for (int i = 0; i < nv; ++i) {
+    if (!V[i]) return NK_EINVAL;
+    A.V[i] = V[i];
+    A.c[i] = coef[i];
+  }
+  A.w = w;
+  A.tau = tau;
+  A.x0 = x0;
+  A.g0 = G0;
+  A.z = z;
+  A.alpha = sc * zs;
+  A.sc = sc;
+  A.k = sh_coef(h, r, k, g);
+  A.out_v = v_out;
+  A.out_w = w_out;
+  const int nval = 2 * nv + 3;
+  if (!dots) {  // no reduction wanted (timing): a persistent partial buffer, no synchronisation
+    static double* buf = nullptr;
+    static int64_t cap = 0;
+    const int64_t need = int64_t(nval) * 65536;
+    if (cap < need) {
+      if (buf) hipFree(buf);
+      buf = nullptr;
+      cap = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&buf), sizeof(double) * need) != hipSuccess)
+        return NK_ENOMEM;
+      cap = need;
+    }
+    A.partial = buf;
+    A.partial_cap = cap;
+    int64_t nw = 0;
+    return hip_rc(arnoldi_launch(A, S(stream), &nw));
+  }
+  return reduce_call(int64_t(65536) * 2048, nval, nval, nval, dots, S(stream),
+                     [&](double* part, int64_t* nb) {
+                       A.partial = part;
+                       A.partial_cap = int64_t(nval) * (65536 + 1);
+                       return arnoldi_launch(A, S(stream), nb);
+                     });
+}
+
 // ------------------------------------------------------------------------------ BLAS-1
 int nk_dot(const double* x, const double* y, int64_t n, double* out, void* stream) {
   if (!x || !y || !out || n < 0) return NK_EINVAL;
@@ -293,7 +344,7 @@ int nk_sh_step(nk_sh* s, const double* u_prev, double* u_next, nk_stats* stats) 
 int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {
   static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
                                          "krylov_mdot", "krylov_combo", "reduce_final", "copy",
-                                         "halo", "user_F", "axpby"};
+                                         "halo", "user_F", "axpby", "arnoldi_fused"};
   if (!s) return NK_EINVAL;
   for (int k = 0; k < K_NKINDS && k < max; ++k) {
     std::memset(out[k].name, 0, sizeof(out[k].name));

@@ -188,6 +188,46 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     const double est = ww - hh;                    // |v_{j+1}|^2 = |w|^2 - |h|^2
     const bool lag_step = more && lag && (!next_is_v || est > kLagMinRatio2 * ww);
     int64_t nblk = 0;
+    if (lag_step && P_.has_fused(j + 1)) {
+      // -- fused: v_{j+1} = tau w - V h, JVP_{j+1} and multi-dot_{j+1} in one pass over V
+      //    (arnoldi.hip).  v_{j+1} lands in the spare vector, which then takes V_[j+1]'s place.
+      const double* z = nullptr;
+      double zs, zn;
+      if (next_is_v) {
+        const double e = std::sqrt(est);
+        zs = 1.0 / e;
+        zn = zs * e;
+      } else {
+        input(j + 1, &z, &zs, &zn);
+      }
+      if (zn != 0.0) {  // a zero augmentation vector maps to zero without an F call: unfused path
+        const double* Vp[kMaxVec];
+        double cc[kMaxVec];
+        for (int i = 0; i <= j; ++i) {
+          Vp[i] = V_[i];
+          cc[i] = U.c[i];
+        }
+        int64_t nw = 0;
+        double* vout = Sv_;
+        rc = P_.fused_step(Vp, cc, j + 1, w, tau, X_, G0_, z, zs, omega_ / zn, vout, V_[j + 2],
+                           &nw);
+        if (rc) return rc;
+        Sv_ = V_[j + 1];
+        V_[j + 1] = vout;
+        zp_[j + 1] = next_is_v ? vout : z;
+        zs_[j + 1] = zs;
+        sig_est[j + 1] = next_is_v ? zs : 0.0;
+        st_->njvp += 1;
+        st_->n_arnoldi += 1;
+        const int np1 = j + 2;
+        rc = E_.reduce_async(nw, 2 * np1 + 1, 2 * np1 + 1, Engine::kSlotMdot);
+        if (!rc) rc = E_.sync();
+        if (rc) return rc;
+        hn_pending = true;
+        ++j;
+        continue;
+      }
+    }
     if (lag_step) {
       // -- v_{j+1} = tau w - V h (no reduction), then step j+1 right away
       rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {

@@ -113,4 +113,31 @@ hipError_t shlin_diag_launch(const double* U, const double* Uo, double k, double
 hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
                         int64_t n, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------------
+// Fused Arnoldi step (arnoldi.hip): update v = tau*w + sum c_i V_i, FD JVP w' of z = v (or of an
+// external z), and the multi-dot of w' and v against V and v, in one launch (periodic grid only).
+constexpr int kArnMaxNV = 28;
+struct ArnoldiArgs {
+  int64_t ny = 0, nx = 0;
+  int nv = 0;                      // basis vectors V_0..V_{nv-1}
+  int strips = 0, nbands = 0, RY = 0;  // set by arnoldi_launch
+  const double* V[kArnMaxNV] = {};
+  double c[kArnMaxNV] = {};        // zero beyond nv
+  const double* w = nullptr;       // previous JVP output
+  double tau = 1.0;
+  const double* x0 = nullptr;      // Newton iterate
+  const double* g0 = nullptr;      // G(x0)
+  const double* z = nullptr;       // JVP input if not the new v (LGMRES augmentation vector)
+  double alpha = 0.0;              // y = x0 + alpha z
+  double sc = 1.0;                 // w' = (G(y) - G0)/sc
+  SHCoef k{};
+  double* out_v = nullptr;         // must not alias w or any V_i
+  double* out_w = nullptr;
+  double* partial = nullptr;       // [(2 nv + 3)][nwaves]
+  int64_t partial_cap = 0;         // doubles available at partial
+};
+bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
+// *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
+hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
+
 }  // namespace nk

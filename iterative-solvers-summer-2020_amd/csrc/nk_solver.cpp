@@ -49,9 +49,12 @@ Engine::Engine(int64_t n_, nk_comm* comm_, hipStream_t s_, bool profile_, int64_
     : n(n_), npad(pad(n_)), comm(comm_), s(s_), profile(profile_) {
   // partial-sum slots: the larger of the Krylov multi-dot and the problem's stencil reductions
   const int64_t kb = krylov_blocks(npad) + 1;
-  const int64_t cap = std::max<int64_t>((2 * kMaxVec + 1) * kb, min_partial);
+  // (at least 64 Ki slots: the fused Arnoldi kernel writes (2 nv + 3) values per wave)
+  const int64_t cap = std::max<int64_t>(std::max<int64_t>((2 * kMaxVec + 1) * kb, min_partial), 1 << 16);
   if (hipMalloc(reinterpret_cast<void**>(&partial_), sizeof(double) * cap) != hipSuccess)
     partial_ = nullptr;
+  else
+    partial_cap_ = cap;
   if (hipMalloc(reinterpret_cast<void**>(&dres_), sizeof(double) * kReduceSlots) != hipSuccess)
     dres_ = nullptr;
   if (hipHostMalloc(reinterpret_cast<void**>(&hres_), sizeof(double) * kReduceSlots, 0) !=
@@ -263,6 +266,7 @@ NewtonKrylov::NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* extern
   Ft_ = v[q++];
   G0_ = v[q++];
   Gt_ = v[q++];
+  Sv_ = v[q++];
   const int nv = o.inner_m + o.outer_k + 1;
   V_.assign(nv, nullptr);
   for (int i = 1; i < nv; ++i) V_[i] = v[q++];

@@ -37,6 +37,7 @@ enum Kind : int {
   K_HALO,
   K_USERF,
   K_AXPBY,
+  K_ARNOLDI,
   K_NKINDS
 };
 
@@ -80,6 +81,7 @@ class Engine {
   int copy(double* dst, const double* src, int64_t n);
 
   double* partial() const { return partial_; }
+  int64_t partial_cap() const { return partial_cap_; }
   const KStat& stat(int k) const { return stats_[k]; }
   void reset_stats();
   int64_t bytes_allocated() const { return bytes_; }
@@ -97,6 +99,7 @@ class Engine {
   double* pool_ = nullptr;
   bool own_pool_ = false;
   double* partial_ = nullptr;
+  int64_t partial_cap_ = 0;
   double* dres_ = nullptr;
   double* hres_ = nullptr;
   int64_t bytes_ = 0;
@@ -151,6 +154,16 @@ struct Problem {
   // May the solver evaluate a JVP it later discards (the step after the last Arnoldi step)?  A
   // user callback must see exactly scipy's F calls, so the generic problem says no.
   virtual bool may_speculate() const { return true; }
+  // Fused Arnoldi step (arnoldi.hip): v = tau w + sum c_i V_i -> out_v, w' = J z -> out_w with
+  // z = v (z == nullptr) or z = the given vector (scale zs, norm-free step sc), and the multi-dot
+  // partials of w' and v against V_0..V_{nv-1}, v; *nwaves = partial columns.
+  virtual bool has_fused(int /*nv*/) const { return false; }
+  virtual int fused_step(const double* const* /*V*/, const double* /*c*/, int /*nv*/,
+                         const double* /*w*/, double /*tau*/, const double* /*x0*/,
+                         const double* /*G0*/, const double* /*z*/, double /*zs*/, double /*sc*/,
+                         double* /*out_v*/, double* /*out_w*/, int64_t* /*nwaves*/) {
+    return NK_EINVAL;
+  }
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
 };
@@ -181,6 +194,7 @@ class NewtonKrylov {
   // vectors
   double *X_ = nullptr, *Xt_ = nullptr, *Fx_ = nullptr, *Ft_ = nullptr, *G0_ = nullptr,
          *Gt_ = nullptr;
+  double* Sv_ = nullptr;  // spare vector: target of the fused update (swapped into V_)
   std::vector<double*> V_;      // V_[0] aliases Fx_ during a solve
   std::vector<double*> outer_;  // LGMRES augmentation ring
   std::vector<double> osig_, orn_;

@@ -2,6 +2,7 @@
 #include "sh_problem.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace nk {
 
@@ -196,6 +197,43 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   A.b = field(z, hz_);
   A.p0 = G0;
   return halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+}
+
+// One launch per Arnoldi step on a single periodic slab with the FD JVP (arnoldi.hip); the slab
+// decomposition keeps the unfused update / JVP / multi-dot (its halo exchange sits between them).
+// NKHIP_FUSED=0 disables it (read per call, so a test can compare both paths in one process).
+bool SHProblem::has_fused(int nv) const {
+  const char* e = std::getenv("NKHIP_FUSED");
+  if (e && e[0] == '0') return false;
+  return !dist() && jvp_mode_ == NK_JVP_FD && arnoldi_supported(nv, ny_, nx_);
+}
+
+int SHProblem::fused_step(const double* const* V, const double* c, int nv, const double* w,
+                          double tau, const double* x0, const double* G0, const double* z,
+                          double zs, double sc, double* out_v, double* out_w, int64_t* nwaves) {
+  ArnoldiArgs A;
+  A.ny = ny_;
+  A.nx = nx_;
+  A.nv = nv;
+  for (int i = 0; i < nv; ++i) {
+    A.V[i] = V[i];
+    A.c[i] = c[i];
+  }
+  A.w = w;
+  A.tau = tau;
+  A.x0 = x0;
+  A.g0 = G0;
+  A.z = z;
+  A.alpha = sc * zs;  // y = x0 + sc*zs*z (KrylovJacobian.matvec, _nonlin.py:1505-1509)
+  A.sc = sc;
+  A.k = c_;
+  A.out_v = out_v;
+  A.out_w = out_w;
+  A.partial = E_.partial();
+  A.partial_cap = E_.partial_cap();
+  // algorithmic bytes: read V (nv), w, x0, G0 (, z); write v, w'
+  const double bytes = 8.0 * double(ny_ * nx_) * (nv + 5 + (z ? 1 : 0));
+  return E_.launch(K_ARNOLDI, bytes, [&] { return arnoldi_launch(A, E_.s, nwaves); });
 }
 
 // ============================================================================================

@@ -9,6 +9,8 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnkhip.so")
+# NKHIP_LIB: an alternative build of the same C-ABI (kernel tuning builds, `make tune`)
+LIB_PATH = os.environ.get("NKHIP_LIB") or LIB_PATH
 
 NK_OK = 0
 NK_NO_CONVERGENCE = 1
@@ -77,6 +79,9 @@ SIGNATURES = [
     ("nk_sh_residual", C.c_int, [_P, _P, _P, _I64, _I64, _D, _D, _D, _D, _P]),
     ("nk_sh_jvp", C.c_int, [_P, _P, _P, _I64, _I64, _D, _D, _D, _D, _P]),
     ("nk_sh_fdjvp", C.c_int, [_P, _P, _P, _P, _I64, _I64, _D, _D, _D, _D, _D, _D, _P]),
+    ("nk_sh_arnoldi_fused", C.c_int, [C.POINTER(_P), C.POINTER(_D), _I32, _P, _D, _P, _P, _P,
+                                      _I64, _I64, _D, _D, _D, _D, _D, _D, _P, _P,
+                                      C.POINTER(_D), _P]),
     ("nk_dot", C.c_int, [_P, _P, _I64, C.POINTER(_D), _P]),
     ("nk_nrm2", C.c_int, [_P, _I64, C.POINTER(_D), _P]),
     ("nk_maxnorm", C.c_int, [_P, _I64, C.POINTER(_D), _P]),

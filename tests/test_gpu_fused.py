@@ -1,0 +1,116 @@
+"""GPU: the fused Arnoldi step (arnoldi.hip) against the unfused update / JVP / multi-dot path.
+
+The fused launch reads the basis once per Arnoldi step; it changes only the summation order of
+the dot products, so both paths must reach the same root (f_tol = 1e-10: agreement to 1e-8 of
+the state's scale) with Newton iteration counts within one.  Shapes cover nx not a multiple of
+the 60-column wave strip, odd nx, non-square grids and a grid whose band count exceeds its rows.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sh_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(ny, nx, fused, ftol=1e-10, seed=2020, steps=1):
+    import nkhip
+    os.environ["NKHIP_FUSED"] = "1" if fused else "0"
+    try:
+        m = nkhip.SwiftHohenberg(N=nx, ny=ny, d=0.625 * nx, f_tol=ftol)
+        U0 = np.random.default_rng(seed).standard_normal((ny, nx))
+        U = torch.as_tensor(U0, device="cuda")
+        stats = []
+        for _ in range(steps):
+            U = m.step(U)
+            stats.append(dict(m.last_stats))
+        prof = m.kernel_profile()
+        m.close()
+    finally:
+        os.environ.pop("NKHIP_FUSED", None)
+    return U0, U.cpu().numpy(), stats, prof
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 64), (61, 61), (96, 130), (40, 256), (128, 60),
+                                   (8, 200), (256, 256)])
+def test_fused_matches_unfused(ny, nx):
+    U0, a, sa, pa = _step(ny, nx, fused=True)
+    _, b, sb, pb = _step(ny, nx, fused=False)
+    assert pa["arnoldi_fused"]["launches"] > 0
+    assert pb["arnoldi_fused"]["launches"] == 0
+    scale = max(1.0, float(np.abs(b).max()))
+    assert float(np.abs(a - b).max()) <= 1e-8 * scale
+    assert abs(sa[0]["nit"] - sb[0]["nit"]) <= 1
+    # the fused path's output is a root of the reference residual (sh_scipy_nk.py:47-49)
+    F = sh_oracle.residual(a.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
+    assert np.abs(F).max() <= 1e-9
+
+
+def test_fused_default_tolerance_and_counts():
+    """Default f_tol at 512^2 over 3 steps: same roots to the solver tolerance, Krylov work
+    within a few percent of the unfused path."""
+    _, a, sa, pa = _step(512, 512, fused=True, ftol=None, steps=3)
+    _, b, sb, pb = _step(512, 512, fused=False, ftol=None, steps=3)
+    scale = max(1.0, float(np.abs(b).max()))
+    assert float(np.abs(a - b).max()) <= 1e-5 * scale
+    for x, y in zip(sa, sb):
+        assert abs(x["nit"] - y["nit"]) <= 1
+    na = sum(s["n_arnoldi"] for s in sa)
+    nb = sum(s["n_arnoldi"] for s in sb)
+    assert abs(na - nb) <= 0.1 * nb + 3
+    # most Arnoldi steps run fused (the unfused ones: first step, short-norm fallbacks)
+    assert pa["arnoldi_fused"]["launches"] >= 0.5 * na
+
+
+def test_fused_deterministic():
+    _, a, _, _ = _step(96, 130, fused=True)
+    _, b, _, _ = _step(96, 130, fused=True)
+    assert np.array_equal(a, b)
+
+
+def _torch_G(y, h, r, k, g):
+    """G(y) = y/k - (L y + g y^2 - y^3)/2 with L = -Lap^2 - 2 Lap + (r-1) I by periodic rolls
+    (sh_scipy_nk.py:32-39,49), an fp64 torch reference independent of the HIP stencils."""
+    e = 1.0 / h ** 2
+
+    def lap(a):
+        return e * (torch.roll(a, 1, 0) + torch.roll(a, -1, 0) + torch.roll(a, 1, 1)
+                    + torch.roll(a, -1, 1) - 4 * a)
+
+    la = lap(y)
+    Ly = -lap(la) - 2 * la + (r - 1) * y
+    return y / k - (Ly + g * y * y - y * y * y) / 2
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 64), (40, 130), (96, 61)])
+@pytest.mark.parametrize("nv", [1, 5, 17, 28])
+@pytest.mark.parametrize("ext", [False, True])
+def test_fused_kernel_vs_torch(ny, nx, nv, ext):
+    import nkhip
+    gen = torch.Generator(device="cpu").manual_seed(nv * 100 + nx)
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    V = [rnd() for _ in range(nv)]
+    coef = [float(c) for c in torch.randn(nv, generator=gen, dtype=torch.float64)]
+    w, x0 = rnd(), rnd()
+    z = rnd() if ext else None
+    h, r, k, g, tau = 0.625, 0.01, 0.2, 1.0, 0.75
+    G0 = _torch_G(x0, h, r, k, g)
+    zs, sc = 0.5, 1e-3
+    v, wo, dots = nkhip.sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=z)
+    vr = tau * w
+    for c, Vi in zip(coef, V):
+        vr = vr + c * Vi
+    zr = z if ext else vr
+    wr = (_torch_G(x0 + sc * zs * zr, h, r, k, g) - G0) / sc
+    assert float((v - vr).abs().max()) <= 1e-13 * float(vr.abs().max())
+    assert float((wo - wr).abs().max()) <= 1e-9 * float(wr.abs().max())
+    ref = [float((wr * Vi).sum()) for Vi in V] + [float((wr * vr).sum())]
+    ref += [float((vr * Vi).sum()) for Vi in V] + [float((vr * vr).sum()), float((wr * wr).sum())]
+    scale_w = float(wr.norm()) * float(max(Vi.norm() for Vi in V + [vr]))
+    scale_v = float(vr.norm()) * float(max(Vi.norm() for Vi in V + [vr]))
+    for i, (a, b) in enumerate(zip(dots, ref)):
+        scale = scale_w if (i <= nv or i == 2 * nv + 2) else scale_v
+        assert abs(a - b) <= 1e-10 * scale, (i, a, b)
