@@ -115,7 +115,8 @@ int nk_sh_fdjvp(const double* x0_dev, const double* G0_dev, const double* z_dev,
  *   v = tau*w + sum_i coef[i]*V[i]                 -> v_out
  *   w' = (G(x0 + sc*zs*z) - G0)/sc,  z = v if z_dev == NULL   -> w_out
  *   dots[0..2nv+2] = [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']  (host; NULL: no reduction,
- *   no synchronisation).  nv <= 32, ny, nx >= 8, periodic grid; v_out must not alias w or V[i]. */
+ *   no synchronisation).  nv <= 35, ny >= 8, nx >= 4 even, 16-B aligned vectors, periodic grid;
+ *   v_out must not alias w or V[i]. */
 int nk_sh_arnoldi_fused(const double* const* V_dev, const double* coef, int32_t nv,
                         const double* w_dev, double tau, const double* x0_dev, const double* G0_dev,
                         const double* z_dev, int64_t ny, int64_t nx, double h, double r, double k,

@@ -58,18 +58,14 @@ __device__ __forceinline__ double ldb(const double* base, uint32_t off) {
 // nothing, so masked stores need no branch.
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(double* p, int64_t n) {
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(uint32_t(n * 8)), 0x00020000);
 }
-__device__ __forceinline__ void stb(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
-}
 
-// Rows of loads in flight per wave for a basis of NV vectors: as many as the registers allow at
-// the occupancy the register count gives (and the 63 loads the wait counter tracks).
-constexpr int pf_for(int nv) {
-  return nv <= 2 ? 4 : nv <= 6 ? 3 : nv <= 16 ? 2 : 1;
-}
+// Rows of loads in flight per wave for a basis of NV vectors (register budget at one or two
+// waves per SIMD; the wait counter tracks at most 63 loads)
+constexpr int pf_for(int nv) { return nv <= 4 ? 3 : nv <= 20 ? 2 : 1; }
 
 __device__ __forceinline__ double readlane(double v, int l) {
   const u32x2 b = __builtin_bit_cast(u32x2, v);
@@ -78,17 +74,54 @@ __device__ __forceinline__ double readlane(double v, int l) {
   r.y = __builtin_amdgcn_readlane(b.y, l);
   return __builtin_bit_cast(double, r);
 }
+// x[lane] + x[lane ^ 32], summed as (lanes 0-31) + (lanes 32-63) in every lane (bitwise equal
+// in both halves), and x[lane ^ 32]: one v_permlane32_swap per 32-bit half
+__device__ __forceinline__ void swap32(double x, double* lo, double* hi) {
+  const u32x2 b = __builtin_bit_cast(u32x2, x);
+  const auto a0 = __builtin_amdgcn_permlane32_swap(b.x, b.x, false, false);
+  const auto a1 = __builtin_amdgcn_permlane32_swap(b.y, b.y, false, false);
+  u32x2 l, h;
+  l.x = a0[0];
+  l.y = a1[0];
+  h.x = a0[1];
+  h.y = a1[1];
+  *lo = __builtin_bit_cast(double, l);  // x of lane (lane & 31)
+  *hi = __builtin_bit_cast(double, h);  // x of lane (lane | 32)
+}
+__device__ __forceinline__ double pair_sum(double x) {
+  double lo, hi;
+  swap32(x, &lo, &hi);
+  return lo + hi;
+}
+__device__ __forceinline__ double partner(double x, int hf) {
+  double lo, hi;
+  swap32(x, &lo, &hi);
+  return hf ? lo : hi;
+}
+typedef double dv2 __attribute__((ext_vector_type(2)));
 
+// Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
+// holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
+//   [V_0 .. V_{NV-1}, w, x0, G0, (z)]
+// in load k, so every load instruction streams two 512-B row segments of two vectors.  The update
+// sums each half's entries and adds the other half's sum (v_permlane32_swap); both halves then
+// hold v, y and w' of the wave's 64 columns, and each half takes the dot products of its own
+// entries (half 0 also w'.v, v.v, w'.w').
 template <int NV, bool EXT, int PF, bool NT>
 __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) {
-  constexpr int RR = PF + 1;  // register ring: the update row r+2 and PF rows in flight
-  // lag rows r, r+1 of the basis (and G0) for the dot products, one region per wave
-  __shared__ double lag[WPB][2][NV + 1][64];
-  // per row (parity slot): y on lanes 0, 1, 62, 63 of every wave; the waves' partial sums of v on
-  // the block's four halo columns
+  constexpr int RR = PF + 1;               // register ring: the update row and PF rows in flight
+  constexpr int NE = NV + 3 + (EXT ? 1 : 0);
+  constexpr int NI = (NE + 1) / 2;         // 16-B loads per row and lane
+  constexpr int NB = (NV + 1) / 2;         // loads holding basis entries
+  constexpr int EX = NV + 1, EG = NV + 2, EZ = NV + 3;  // entries of x0, G0, z
+  // lag rows r, r+1 of this lane's basis entries and of G0, for row r's dot products / stencil
+  __shared__ dv2 lag[WPB][2][NB + 1][64];
+  // per row (parity slot): y on columns 0, 1, 62, 63 of every wave; the waves' partial sums of v
+  // on the block's four halo columns
   __shared__ double edge[2][WPB][4];
   __shared__ double hpart[2][WPB][4];
   const int lane = threadIdx.x & 63;
+  const int hf = lane >> 5, l = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware mapping: consecutive blocks go round-robin over the 8 XCDs; give each XCD one
   // contiguous run of blocks (whole bands), so band halos are shared inside one L2.
@@ -100,9 +133,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const int64_t band = L / ngroups, grp = L % ngroups;
   const int64_t gw = L * WPB + wid;  // partial-sum column of this wave
   const int64_t nx = A.nx, ny = A.ny;
-  const int64_t B0 = grp * WPB * kSW;  // the block's first column
-  const int64_t c = B0 + wid * kSW + lane;  // columns past nx compute wrapped columns, masked
-  const int64_t col = c % nx;
+  const int64_t B0 = grp * WPB * kSW;        // the block's first column
+  const int64_t c = B0 + wid * kSW + 2 * l;  // columns past nx compute wrapped columns, masked
+  const int64_t col = c % nx;                // nx even: c and c+1 wrap together
   const bool own = c < nx;
   // block halo: h = 0, 1 -> columns B0-2, B0-1; h = 2, 3 -> B0 + WPB*64, +1
   const int hh = lane & 3;
@@ -115,10 +148,29 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const double isc = 1.0 / A.sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
-  double (*lg)[NV + 1][64] = lag[wid];
-  // packed block-halo loads, shared by the WPB waves: lane L of wave w fetches halo column L%4 of
-  // entry e = w + WPB*(L/4) of [V_0 .. V_{NV-1}, w] with coefficient c_e (tau for w); lanes past
-  // the list repeat entry w's address (same cache line, no extra traffic) with coefficient 0
+  dv2 (*lg)[NB + 1][64] = lag[wid];
+
+  // per-lane source of load k (entry 2k + hf) and its update coefficient; the padding entry
+  // (NE odd) repeats the other half's address with coefficient 0
+  const double* ep[NI];
+  double ecf[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    auto src = [&](int e) -> const double* {
+      if (e < NV) return A.V[e];
+      if (e == NV) return A.w;
+      if (e == EX) return A.x0;
+      if (e == EG) return A.g0;
+      return EXT ? A.z : A.g0;
+    };
+    auto cof = [&](int e) -> double { return e < NV ? A.c[e] : (e == NV ? A.tau : 0.0); };
+    const int e0 = 2 * k, e1 = (2 * k + 1 < NE) ? 2 * k + 1 : 2 * k;
+    ep[k] = hf ? src(e1) : src(e0);
+    ecf[k] = hf ? (2 * k + 1 < NE ? cof(e1) : 0.0) : cof(e0);
+  }
+  // packed block-halo loads (8 B per lane), shared by the WPB waves: lane L of wave w fetches
+  // halo column L%4 of entry e = w + WPB*(L/4) of [V_0 .. V_{NV-1}, w] with coefficient c_e (tau
+  // for w); lanes past the list repeat entry w's address (same line) with coefficient 0
   const double* hp;
   double hcf;
   {
@@ -143,43 +195,65 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   };
 
   struct Slot {
-    double v[NV];
-    double w, x, z, g;
+    dv2 e[NI];
     double hv, hx;
   };
   auto load = [&](Slot& s, int64_t q) {
     const int64_t qq = wrap(q);
-    const uint32_t o = uint32_t((qq * nx + col) * 8);
+    const int64_t o = qq * nx + col;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) s.v[i] = ldb<NT>(A.V[i], o);
-    s.w = ldb<NT>(A.w, o);
-    s.x = ldb<NT>(A.x0, o);
-    if constexpr (EXT) s.z = ldb<NT>(A.z, o);
-    s.g = ldb<NT>(A.g0, o);
+    for (int k = 0; k < NI; ++k) {
+      const dv2* p = reinterpret_cast<const dv2*>(ep[k] + o);
+      if constexpr (NT)
+        s.e[k] = __builtin_nontemporal_load(p);
+      else
+        s.e[k] = *p;
+    }
     const int64_t ho = qq * nx + hcol;
     if constexpr (!EXT) s.hv = hp[ho];
     s.hx = hxp[ho];
   };
-  // the basis row and G0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
-  auto stash = [&](const Slot& s, int64_t q) {
-    double (*d)[64] = lg[(q - r0) & 1];
+  // entry e of this row for both halves (e is a compile-time index)
+  auto both = [&](const Slot& s, int e) -> dv2 {
+    const dv2 x = s.e[e / 2];
+    // the swaps run in every lane (a cross-lane read from lanes a branch switched off returns
+    // stale registers), then each half selects
+    const double px = partner(x.x, hf), py = partner(x.y, hf);
+    const bool mine = hf == (e & 1);
+    return dv2{mine ? x.x : px, mine ? x.y : py};
+  };
+  // the basis entries and G0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
+  auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
+    dv2 (*d)[64] = lg[(q - r0) & 1];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) d[i][lane] = s.v[i];
-    d[NV][lane] = s.g;
+    for (int k = 0; k < NB; ++k) d[k][lane] = s.e[k];
+    d[NB][lane] = g;
   };
 
-  // 5-row window (rows r-2 .. r+2): y, the horizontal pair sums h1 = y[c-1] + y[c+1] and
-  // h2 = y[c-2] + y[c+2], and v
-  double yw[5], hw[5], h2w[5], vw[5];
+  // 5-row window (rows r-2 .. r+2) of y, h1 = y[c-1] + y[c+1] and v, two columns per lane
+  dv2 yw[5], hw[5], vw[5];
 #pragma unroll
-  for (int m = 0; m < 5; ++m) yw[m] = hw[m] = h2w[m] = vw[m] = 0.0;
+  for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
+  dv2 gq{0.0, 0.0};  // G0 of the last pushed row (both halves)
   auto push = [&](const Slot& s, int64_t q) {
-    double v = A.tau * s.w;
+    double p0 = 0.0, p1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v += A.c[i] * s.v[i];
-    const double y = s.x + A.alpha * (EXT ? s.z : v);
+    for (int k = 0; k < NI; ++k) {
+      p0 += ecf[k] * s.e[k].x;
+      p1 += ecf[k] * s.e[k].y;
+    }
+    const dv2 v{pair_sum(p0), pair_sum(p1)};
+    const dv2 x0 = both(s, EX);
+    gq = both(s, EG);
+    dv2 y;
+    if constexpr (EXT) {
+      const dv2 z = both(s, EZ);
+      y = dv2{x0.x + A.alpha * z.x, x0.y + A.alpha * z.y};
+    } else {
+      y = dv2{x0.x + A.alpha * v.x, x0.y + A.alpha * v.y};
+    }
     // block halo: this wave's share of c_i V_i on the four halo columns (sum over the 16 lanes
-    // of each column), exchanged with y on the edge lanes of every wave through LDS
+    // of each column), exchanged with y on the edge columns of every wave through LDS
     const int slot = int(q & 1);
     if constexpr (!EXT) {
       double hs = hcf * s.hv;
@@ -189,8 +263,14 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       hs += __shfl_xor(hs, 32, 64);
       if (lane < 4) hpart[slot][wid][lane] = hs;
     }
-    const int el = (lane < 2) ? lane : lane - 60;  // lanes 0, 1, 62, 63 -> 0..3
-    if (lane < 2 || lane >= 62) edge[slot][wid][el] = y;
+    if (lane == 0) {
+      edge[slot][wid][0] = y.x;
+      edge[slot][wid][1] = y.y;
+    }
+    if (lane == 31) {
+      edge[slot][wid][2] = y.x;
+      edge[slot][wid][3] = y.y;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -207,105 +287,139 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const double yl1 = (wid == 0) ? readlane(yh, 1) : edge[slot][wl][3];
     const double yr1 = (wid == WPB - 1) ? readlane(yh, 2) : edge[slot][wr][0];
     const double yr2 = (wid == WPB - 1) ? readlane(yh, 3) : edge[slot][wr][1];
-    const double su1 = __shfl_up(y, 1, 64), sd1 = __shfl_down(y, 1, 64);
-    const double su2 = __shfl_up(y, 2, 64), sd2 = __shfl_down(y, 2, 64);
-    const double l1 = (lane == 0) ? yl1 : su1;
-    const double r1v = (lane == 63) ? yr1 : sd1;
-    const double l2 = (lane == 0) ? yl2 : ((lane == 1) ? yl1 : su2);
-    const double r2v = (lane == 63) ? yr2 : ((lane == 62) ? yr1 : sd2);
+    // neighbours inside the half (width 32): lane l-1 holds columns 2l-2, 2l-1
+    const double ux = __shfl_up(y.x, 1, 32), uy = __shfl_up(y.y, 1, 32);
+    const double dx = __shfl_down(y.x, 1, 32), dy = __shfl_down(y.y, 1, 32);
+    const double cm2 = (l == 0) ? yl2 : ux, cm1 = (l == 0) ? yl1 : uy;   // columns 2l-2, 2l-1
+    const double cp2 = (l == 31) ? yr1 : dx, cp3 = (l == 31) ? yr2 : dy;  // columns 2l+2, 2l+3
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       yw[m] = yw[m + 1];
       hw[m] = hw[m + 1];
-      h2w[m] = h2w[m + 1];
       vw[m] = vw[m + 1];
     }
     yw[4] = y;
-    hw[4] = l1 + r1v;
-    h2w[4] = l2 + r2v;
+    hw[4] = dv2{cm1 + y.y, y.x + cp2};
     vw[4] = v;
-    const bool st = own && q >= r0 && q < r1;
-    stb(rv, st ? uint32_t((q * nx + col) * 8) : kOOB, v);
+    // the h2 = y[c-2] + y[c+2] of row q is needed only when q is the window centre: keep the
+    // four outer neighbours of the row two steps back
+    const bool st = own && hf == 0 && q >= r0 && q < r1;
+    const __amdgpu_buffer_rsrc_t r = rv;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
+                                           st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
+    return dv2{cm2 + cp2, cm1 + cp3};  // h2 of row q
   };
 
-  double aw[NV], ag[NV];
+  double aw[NB], ag[NB];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) aw[i] = ag[i] = 0.0;
+  for (int k = 0; k < NB; ++k) aw[k] = ag[k] = 0.0;
   double awn = 0.0, avv = 0.0, aww = 0.0;
-  // stencil + dot products of row r (window centre = row r; basis row r from LDS)
-  auto centre = [&](int64_t r) {
-    const double (*d)[64] = lg[(r - r0) & 1];
-    const double yc = yw[2];
-    const double a1 = hw[2] + (yw[1] + yw[3]);
-    const double dg = hw[1] + hw[3];
-    const double a2 = h2w[2] + (yw[0] + yw[4]);
-    const double Ly = applyL13(K, yc, a1, dg, a2);
-    const double yy = yc * yc;
-    const double G = yc / K.k - (Ly + K.g * yy - yc * yy) / 2;
-    const double wo = (G - d[NV][lane]) * isc;
-    const bool in = own && r < r1;
-    stb(rw, in ? uint32_t((r * nx + col) * 8) : kOOB, wo);
-    const double wm = in ? wo : 0.0;
-    const double vm = in ? vw[2] : 0.0;
+  dv2 h2w[3];  // h2 of rows r, r+1, r+2
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const double bi = d[i][lane];
-      aw[i] += wm * bi;
-      ag[i] += vm * bi;
+  for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
+  // stencil + dot products of row r (window centre = row r; basis row r and G0 from LDS)
+  auto centre = [&](int64_t r) {
+    const dv2 (*d)[64] = lg[(r - r0) & 1];
+    const dv2 g = d[NB][lane];
+    dv2 wo;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double yc = yw[2][q];
+      const double a1 = hw[2][q] + (yw[1][q] + yw[3][q]);
+      const double dg = hw[1][q] + hw[3][q];
+      const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
+      const double Ly = applyL13(K, yc, a1, dg, a2);
+      const double yy = yc * yc;
+      const double G = yc / K.k - (Ly + K.g * yy - yc * yy) / 2;
+      wo[q] = (G - g[q]) * isc;
     }
-    awn += wm * vm;
-    avv += vm * vm;
-    aww += wm * wm;
+    const bool in = own && r < r1;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
+                                           (in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB,
+                                           0, 0);
+    const dv2 wm = in ? wo : dv2{0.0, 0.0};
+    const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const dv2 bi = d[k][lane];
+      aw[k] += wm.x * bi.x + wm.y * bi.y;
+      ag[k] += vm.x * bi.x + vm.y * bi.y;
+    }
+    const double h0 = hf ? 0.0 : 1.0;  // the three squares once per column (half 0)
+    awn += h0 * (wm.x * vm.x + wm.y * vm.y);
+    avv += h0 * (vm.x * vm.x + vm.y * vm.y);
+    aww += h0 * (wm.x * wm.x + wm.y * wm.y);
+  };
+  auto push_h2 = [&](const Slot& s, int64_t q) {
+    const dv2 h2 = push(s, q);
+    h2w[0] = h2w[1];
+    h2w[1] = h2w[2];
+    h2w[2] = h2;
   };
 
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
     // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
-    // (q - r0 - 2) mod RR.
-    // (at most max(4, 2 + PF) rows of loads live at once: the register peak of the kernel)
-    Slot P[4];
+    // (q - r0 - 2) mod RR.  At most 2 + PF rows of loads are live at once.
+    {
+      Slot P[2];
+      load(P[0], r0 - 2);
+      load(P[1], r0 - 1);
+      push_h2(P[0], r0 - 2);
+      push_h2(P[1], r0 - 1);
+      load(P[0], r0);
+      load(P[1], r0 + 1);
+      Slot S[RR];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) load(P[d], r0 - 2 + d);
-    push(P[0], r0 - 2);
-    push(P[1], r0 - 1);
-    Slot S[RR];
+      for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
+      push_h2(P[0], r0);
+      stash(P[0], gq, r0);
+      push_h2(P[1], r0 + 1);
+      stash(P[1], gq, r0 + 1);
+      // whole groups of RR rows with no branch inside the group (a branch would make the
+      // compiler's wait-count analysis drain every load in flight): rows past the band end
+      // are computed on clamped rows and masked out of the stores and sums
+      for (int64_t t0 = 0; t0 < nrows; t0 += RR) {
 #pragma unroll
-    for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
-    push(P[2], r0);
-    push(P[3], r0 + 1);
-    stash(P[2], r0);
-    stash(P[3], r0 + 1);
-    // whole groups of RR rows with no branch inside the group (a branch would make the
-    // compiler's wait-count analysis drain every load in flight): rows past the band end are
-    // computed on clamped rows and masked out of the stores and sums
-    for (int64_t t0 = 0; t0 < nrows; t0 += RR) {
-#pragma unroll
-      for (int k = 0; k < RR; ++k) {
-        const int64_t r = r0 + t0 + k;
-        load(S[(k + PF) % RR], r + 2 + PF);  // the slot of row r+1, consumed last step
-        push(S[k], r + 2);
-        centre(r);
-        stash(S[k], r + 2);  // into the LDS slot row r just vacated
+        for (int k = 0; k < RR; ++k) {
+          const int64_t r = r0 + t0 + k;
+          load(S[(k + PF) % RR], r + 2 + PF);  // the slot of row r+1, consumed last step
+          push_h2(S[k], r + 2);
+          centre(r);
+          stash(S[k], gq, r + 2);  // into the LDS slot row r just vacated
+        }
       }
     }
   }
 
-  // one partial per wave: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
-  wave_sum<NV>(aw);
-  wave_sum<NV>(ag);
+  // one partial per wave: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']; entry 2k + hf of
+  // load k is summed over its half (width-32 butterflies)
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      aw[k] += __shfl_xor(aw[k], o, 64);
+      ag[k] += __shfl_xor(ag[k], o, 64);
+    }
+  }
   double t3[3] = {awn, avv, aww};
   wave_sum<3>(t3);
-  if (lane == 0) {
+  if (l == 0) {
     const int64_t nw = ngroups * WPB * A.nbands;  // every wave of every block writes a column
     double* p = A.partial + gw;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      p[int64_t(i) * nw] = aw[i];
-      p[int64_t(NV + 1 + i) * nw] = ag[i];
+    for (int k = 0; k < NB; ++k) {
+      const int e = 2 * k + hf;
+      if (e < NV) {
+        p[int64_t(e) * nw] = aw[k];
+        p[int64_t(NV + 1 + e) * nw] = ag[k];
+      }
     }
-    p[int64_t(NV) * nw] = t3[0];
-    p[int64_t(2 * NV + 1) * nw] = t3[1];
-    p[int64_t(2 * NV + 2) * nw] = t3[2];
+    if (hf == 0) {
+      p[int64_t(NV) * nw] = t3[0];
+      p[int64_t(2 * NV + 1) * nw] = t3[1];
+      p[int64_t(2 * NV + 2) * nw] = t3[2];
+    }
   }
 }
 
@@ -390,12 +504,16 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
 
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx) {
   static const int maxnv = env_int("NKHIP_ARN_MAXNV", kArnMaxNV);
-  return nv >= 1 && nv <= kArnMaxNV && nv <= maxnv && ny >= 8 && nx >= 4 &&
+  return nv >= 1 && nv <= kArnMaxNV && nv <= maxnv && ny >= 8 && nx >= 4 && nx % 2 == 0 &&
          ny * nx * 8 < (int64_t(1) << 32);  // 32-bit byte offsets
 }
 
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   if (!arnoldi_supported(A.nv, A.ny, A.nx)) return hipErrorInvalidValue;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  bool al = al16(A.w) && al16(A.x0) && al16(A.g0) && al16(A.z) && al16(A.out_v) && al16(A.out_w);
+  for (int i = 0; i < A.nv; ++i) al = al && al16(A.V[i]);
+  if (!al) return hipErrorInvalidValue;  // 16-B loads and stores
   if (A.z) return launch_e<true>(A, s, nwaves);
   return launch_e<false>(A, s, nwaves);
 }

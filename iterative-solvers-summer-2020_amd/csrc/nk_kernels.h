@@ -116,7 +116,7 @@ hipError_t axpby_launch(double a, const double* x, double b, const double* y, do
 // ---------------------------------------------------------------------------------------------
 // Fused Arnoldi step (arnoldi.hip): update v = tau*w + sum c_i V_i, FD JVP w' of z = v (or of an
 // external z), and the multi-dot of w' and v against V and v, in one launch (periodic grid only).
-constexpr int kArnMaxNV = 28;
+constexpr int kArnMaxNV = 35;
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;
   int nv = 0;                      // basis vectors V_0..V_{nv-1}

@@ -17,7 +17,7 @@ import nkhip  # noqa: E402
 
 def main():
     N = int(os.environ.get("ARN_N", "4096"))
-    nvs = [int(x) for x in os.environ.get("ARN_NVS", "1,4,8,12,16,20,24,28").split(",")]
+    nvs = [int(x) for x in os.environ.get("ARN_NVS", "1,4,8,12,16,20,24,28,32,35").split(",")]
     n = N * N
     torch.manual_seed(0)
     V = [torch.randn(N, N, dtype=torch.float64, device="cuda") for _ in range(max(nvs))]

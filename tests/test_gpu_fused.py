@@ -35,11 +35,14 @@ def _step(ny, nx, fused, ftol=1e-10, seed=2020, steps=1):
 
 
 @pytest.mark.parametrize("ny,nx", [(64, 64), (61, 61), (96, 130), (40, 256), (128, 60),
-                                   (8, 200), (256, 256)])
+                                   (8, 200), (256, 256), (12, 6)])
 def test_fused_matches_unfused(ny, nx):
     U0, a, sa, pa = _step(ny, nx, fused=True)
     _, b, sb, pb = _step(ny, nx, fused=False)
-    assert pa["arnoldi_fused"]["launches"] > 0
+    if nx % 2 == 0:
+        assert pa["arnoldi_fused"]["launches"] > 0
+    else:  # the fused kernel streams column pairs: odd nx keeps the unfused path
+        assert pa["arnoldi_fused"]["launches"] == 0
     assert pb["arnoldi_fused"]["launches"] == 0
     scale = max(1.0, float(np.abs(b).max()))
     assert float(np.abs(a - b).max()) <= 1e-8 * scale
@@ -85,8 +88,8 @@ def _torch_G(y, h, r, k, g):
     return y / k - (Ly + g * y * y - y * y * y) / 2
 
 
-@pytest.mark.parametrize("ny,nx", [(64, 64), (40, 130), (96, 61)])
-@pytest.mark.parametrize("nv", [1, 5, 17, 28])
+@pytest.mark.parametrize("ny,nx", [(64, 64), (40, 130), (96, 62), (16, 4)])
+@pytest.mark.parametrize("nv", [1, 5, 18, 35])
 @pytest.mark.parametrize("ext", [False, True])
 def test_fused_kernel_vs_torch(ny, nx, nv, ext):
     import nkhip
