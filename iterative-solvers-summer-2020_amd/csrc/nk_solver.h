@@ -61,7 +61,15 @@ class Engine {
   // Allocate `count` zeroed vectors of npad doubles from one pool (or carve from `external`).
   int alloc(int count, std::vector<double*>* out, void* external = nullptr,
             int64_t external_bytes = 0);
-  static int64_t pad(int64_t n) { return (n + 255) / 256 * 256; }
+  // Vector stride in the pool.  Large vectors get an odd multiple of 128 KiB: consecutive basis
+  // vectors read at the same offset then spread over the HBM channels instead of landing on the
+  // same ones (scripts/micro/march_bench.hip, 24 vectors of 4096^2 streamed row by row: pool
+  // stride 2^27 B 5.2-5.6 TB/s, 2^27 + 2^17 B 6.4-6.5 TB/s; contiguous chunks 6.0 -> 6.6 TB/s).
+  static int64_t pad(int64_t n) {
+    const int64_t p = (n + 255) / 256 * 256;
+    if (p < (int64_t(1) << 16)) return p;
+    return (p + 32767) / 32768 * 32768 + 16384;
+  }
 
   template <class L>
   int launch(int kind, double bytes, L&& fn);

@@ -13,8 +13,8 @@ step() {  # step <name> <timeout-seconds> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests)  step pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
-    alltests) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    tests)  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ;;
+    alltests) step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 900 python bench.py --steps 5 --warmup 1 --cpu-baseline off --extra off ;;
     benchfull) step bench_full 900 python bench.py ;;
