@@ -188,6 +188,10 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     hcf = cf;
   }
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
+  // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their y arrives in A.yh (the x0 entry
+  // and the x0 halo lanes read it there, and the row's update / z term is dropped)
+  const bool slab = A.yh != nullptr;
+  const double* yhb = slab ? A.yh : A.x0;
 
   auto wrap = [&](int64_t q) -> int64_t {
     q = (q > r1 + 1) ? r1 + 1 : q;  // past the band halo: re-read its last row
@@ -197,13 +201,19 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   struct Slot {
     dv2 e[NI];
     double hv, hx;
+    bool own;  // row of this slab (false: a neighbour's halo row, y taken from A.yh)
   };
   auto load = [&](Slot& s, int64_t q) {
     const int64_t qq = wrap(q);
     const int64_t o = qq * nx + col;
+    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
+    const bool hrow = slab && (qc < 0 || qc >= ny);
+    const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-      const dv2* p = reinterpret_cast<const dv2*>(ep[k] + o);
+      const double* a = ep[k] + o;
+      if (k == EX / 2) a = (hrow && hf == (EX & 1)) ? yhb + hq * nx + col : a;
+      const dv2* p = reinterpret_cast<const dv2*>(a);
       if constexpr (NT)
         s.e[k] = __builtin_nontemporal_load(p);
       else
@@ -211,7 +221,8 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     }
     const int64_t ho = qq * nx + hcol;
     if constexpr (!EXT) s.hv = hp[ho];
-    s.hx = hxp[ho];
+    s.hx = *((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
+    s.own = !hrow;
   };
   // entry e of this row for both halves (e is a compile-time index)
   auto both = [&](const Slot& s, int e) -> dv2 {
@@ -247,10 +258,12 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     gq = both(s, EG);
     dv2 y;
     if constexpr (EXT) {
-      const dv2 z = both(s, EZ);
+      const dv2 z0 = both(s, EZ);
+      const dv2 z = s.own ? z0 : dv2{0.0, 0.0};
       y = dv2{x0.x + A.alpha * z.x, x0.y + A.alpha * z.y};
     } else {
-      y = dv2{x0.x + A.alpha * v.x, x0.y + A.alpha * v.y};
+      const dv2 u = s.own ? v : dv2{0.0, 0.0};
+      y = dv2{x0.x + A.alpha * u.x, x0.y + A.alpha * u.y};
     }
     // block halo: this wave's share of c_i V_i on the four halo columns (sum over the 16 lanes
     // of each column), exchanged with y on the edge columns of every wave through LDS
@@ -281,7 +294,8 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 #pragma unroll
       for (int w = 0; w < WPB; ++w) hz += hpart[slot][w][hh];  // fixed order: deterministic
     }
-    const double yh = s.hx + A.alpha * hz;  // lanes 0..3: block halo columns -2, -1, +0, +1
+    // lanes 0..3: block halo columns -2, -1, +0, +1
+    const double yh = s.hx + A.alpha * (s.own ? hz : 0.0);
     const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WPB - 1) ? wid + 1 : WPB - 1;
     const double yl2 = (wid == 0) ? readlane(yh, 0) : edge[slot][wl][2];
     const double yl1 = (wid == 0) ? readlane(yh, 1) : edge[slot][wl][3];
@@ -500,7 +514,39 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   }
 }
 
+// y on the edge rows 0, 1, ny-2, ny-1 of a slab (grid: column blocks x 4 rows).  The update sum
+// runs in the fused kernel's order -- entries 0, 2, 4, .. of [V_0 .. V_{nv-1}, w] in one partial,
+// 1, 3, 5, .. in the other, then their sum -- so a halo row equals the row its owner computes.
+__global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4) {
+  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= A.nx) return;
+  const int t = blockIdx.y;
+  const int64_t row = (t < 2) ? t : A.ny - 4 + t;
+  const int64_t o = row * A.nx + j;
+  double y;
+  if (A.z) {
+    y = A.x0[o] + A.alpha * A.z[o];
+  } else {
+    double p[2] = {0.0, 0.0};
+    for (int e = 0; e <= A.nv; ++e) {
+      const double x = (e < A.nv) ? A.V[e][o] : A.w[o];
+      const double c = (e < A.nv) ? A.c[e] : A.tau;
+      p[e & 1] += c * x;
+    }
+    const double v = p[0] + p[1];
+    y = A.x0[o] + A.alpha * v;
+  }
+  y4[int64_t(t) * A.nx + j] = y;
+}
+
 }  // namespace
+
+hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) {
+  if (A.ny < 4 || A.nx < 1 || !y4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(arnoldi_edge_kernel, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256), 0, s,
+                     A, y4);
+  return hipGetLastError();
+}
 
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx) {
   static const int maxnv = env_int("NKHIP_ARN_MAXNV", kArnMaxNV);

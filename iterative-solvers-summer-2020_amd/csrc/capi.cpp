@@ -344,7 +344,8 @@ int nk_sh_step(nk_sh* s, const double* u_prev, double* u_next, nk_stats* stats) 
 int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {
   static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
                                          "krylov_mdot", "krylov_combo", "reduce_final", "copy",
-                                         "halo", "user_F", "axpby", "arnoldi_fused"};
+                                         "halo", "user_F", "axpby", "arnoldi_fused",
+                                         "arnoldi_edge"};
   if (!s) return NK_EINVAL;
   for (int k = 0; k < K_NKINDS && k < max; ++k) {
     std::memset(out[k].name, 0, sizeof(out[k].name));

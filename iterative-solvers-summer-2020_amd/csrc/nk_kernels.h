@@ -133,11 +133,17 @@ struct ArnoldiArgs {
   SHCoef k{};
   double* out_v = nullptr;         // must not alias w or any V_i
   double* out_w = nullptr;
+  // row slab (one of several): y on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
+  // arnoldi_edge_launch on every rank + the halo exchange); nullptr = single periodic slab
+  const double* yh = nullptr;
   double* partial = nullptr;       // [(2 nv + 3)][nwaves]
   int64_t partial_cap = 0;         // doubles available at partial
 };
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
+// y = x0 + alpha v (or alpha z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
+// with the fused kernel's summation order: what the neighbours need as their halo rows
+hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
 
 }  // namespace nk

@@ -38,6 +38,7 @@ enum Kind : int {
   K_USERF,
   K_AXPBY,
   K_ARNOLDI,
+  K_ARN_EDGE,
   K_NKINDS
 };
 

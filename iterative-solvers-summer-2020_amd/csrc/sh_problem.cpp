@@ -23,7 +23,7 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
       return;
     }
     double* h = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&h), sizeof(double) * 16 * nx) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&h), sizeof(double) * 24 * nx) != hipSuccess) {
       status_ = NK_ENOMEM;
       return;
     }
@@ -31,6 +31,20 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
     hz_ = h + 4 * nx;
     hd_ = h + 8 * nx;
     hu_ = h + 12 * nx;
+    y4_ = h + 16 * nx;
+    yh_ = h + 20 * nx;
+    // every rank must take the fused Arnoldi path or none: decide on the smallest and the
+    // largest slab (one all-reduce; every rank constructs its problem)
+    double mm[2] = {-double(ny), double(ny)};
+    if (hipMemcpyAsync(y4_, mm, sizeof(mm), hipMemcpyHostToDevice, E_.s) != hipSuccess ||
+        E_.comm->allreduce(y4_, 0, 2, E_.s) != NK_OK ||
+        hipMemcpyAsync(mm, y4_, sizeof(mm), hipMemcpyDeviceToHost, E_.s) != hipSuccess ||
+        hipStreamSynchronize(E_.s) != hipSuccess) {
+      status_ = NK_ECOMM;
+      return;
+    }
+    ny_min_ = int64_t(-mm[0]);
+    ny_max_ = int64_t(mm[1]);
     if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming) != hipSuccess) {
@@ -199,13 +213,16 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   return halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
 }
 
-// One launch per Arnoldi step on a single periodic slab with the FD JVP (arnoldi.hip); the slab
-// decomposition keeps the unfused update / JVP / multi-dot (its halo exchange sits between them).
+// One launch per Arnoldi step with the FD JVP (arnoldi.hip).  On a row slab the kernel needs y
+// on the neighbours' two edge rows: every rank first evaluates y on its own edge rows (a 4-row
+// launch), exchanges them, then runs the fused pass with those rows as its halo.
 // NKHIP_FUSED=0 disables it (read per call, so a test can compare both paths in one process).
 bool SHProblem::has_fused(int nv) const {
   const char* e = std::getenv("NKHIP_FUSED");
   if (e && e[0] == '0') return false;
-  return !dist() && jvp_mode_ == NK_JVP_FD && arnoldi_supported(nv, ny_, nx_);
+  if (jvp_mode_ != NK_JVP_FD) return false;
+  if (!dist()) return arnoldi_supported(nv, ny_, nx_);
+  return arnoldi_supported(nv, ny_min_, nx_) && arnoldi_supported(nv, ny_max_, nx_);
 }
 
 int SHProblem::fused_step(const double* const* V, const double* c, int nv, const double* w,
@@ -231,6 +248,18 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   A.out_w = out_w;
   A.partial = E_.partial();
   A.partial_cap = E_.partial_cap();
+  if (dist()) {
+    // edge rows of y -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
+    const double eb = 8.0 * 4 * nx_ * (z ? 3 : nv + 3);
+    int rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
+    if (rc) return rc;
+    rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
+      return E_.comm->halo(y4_, yh_, yh_ + 2 * nx_, 4, nx_, E_.s) == NK_OK ? hipSuccess
+                                                                         : hipErrorUnknown;
+    });
+    if (rc) return NK_ECOMM;
+    A.yh = yh_;
+  }
   // algorithmic bytes: read V (nv), w, x0, G0 (, z); write v, w'
   const double bytes = 8.0 * double(ny_ * nx_) * (nv + 5 + (z ? 1 : 0));
   return E_.launch(K_ARNOLDI, bytes, [&] { return arnoldi_launch(A, E_.s, nwaves); });
