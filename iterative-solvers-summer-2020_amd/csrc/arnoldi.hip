@@ -36,6 +36,16 @@
 namespace nk {
 namespace {
 
+#ifndef ARN_DPPHALO
+#define ARN_DPPHALO 1
+#endif
+#ifndef ARN_SELECT
+#define ARN_SELECT 1
+#endif
+#ifndef ARN_DPPNB
+#define ARN_DPPNB 1
+#endif
+
 constexpr int kSW = 64;  // columns per wave (one per lane)
 constexpr int WPB = 4;   // waves per block
 
@@ -93,12 +103,49 @@ __device__ __forceinline__ double pair_sum(double x) {
   swap32(x, &lo, &hi);
   return lo + hi;
 }
+// x of row (row & ~1) + x of row (row | 1) for the lane's 16-lane row (v_permlane16_swap)
+__device__ __forceinline__ double pair16_sum(double x) {
+  const u32x2 b = __builtin_bit_cast(u32x2, x);
+  const auto a0 = __builtin_amdgcn_permlane16_swap(b.x, b.x, false, false);
+  const auto a1 = __builtin_amdgcn_permlane16_swap(b.y, b.y, false, false);
+  u32x2 l, h;
+  l.x = a0[0];
+  l.y = a1[0];
+  h.x = a0[1];
+  h.y = a1[1];
+  return __builtin_bit_cast(double, l) + __builtin_bit_cast(double, h);
+}
 __device__ __forceinline__ double partner(double x, int hf) {
   double lo, hi;
   swap32(x, &lo, &hi);
   return hf ? lo : hi;
 }
 typedef double dv2 __attribute__((ext_vector_type(2)));
+
+// lane i <- lane i-1 (wave_shr:1) and lane i <- lane i+1 (wave_shl:1); lanes 0 / 63 get 0
+__device__ __forceinline__ double dpp_up(double x) {
+  const u32x2 b = __builtin_bit_cast(u32x2, x);
+  u32x2 r;
+  r.x = __builtin_amdgcn_update_dpp(0u, b.x, 0x138, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp(0u, b.y, 0x138, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+template <int N>  // lane i <- lane i-N inside its 16-lane row (row_shr:N); 0 past the row start
+__device__ __forceinline__ double dpp_row_shr_t(double x) {
+  const u32x2 b = __builtin_bit_cast(u32x2, x);
+  u32x2 r;
+  r.x = __builtin_amdgcn_update_dpp(0u, b.x, 0x110 + N, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp(0u, b.y, 0x110 + N, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+#define dpp_row_shr(x, n) dpp_row_shr_t<n>(x)
+__device__ __forceinline__ double dpp_down(double x) {
+  const u32x2 b = __builtin_bit_cast(u32x2, x);
+  u32x2 r;
+  r.x = __builtin_amdgcn_update_dpp(0u, b.x, 0x130, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp(0u, b.y, 0x130, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
 
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
@@ -269,12 +316,23 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     // of each column), exchanged with y on the edge columns of every wave through LDS
     const int slot = int(q & 1);
     if constexpr (!EXT) {
+      // lane 4e + hh holds entry e (16 per instruction) of halo column hh: sum the four entries
+      // of each 16-lane row (DPP row shifts), then the rows in pairs (permlane16/32 swaps);
+      // lanes 12..15 end with the totals
       double hs = hcf * s.hv;
+#if ARN_DPPHALO
+      hs += dpp_row_shr(hs, 4);
+      hs += dpp_row_shr(hs, 8);
+      hs = pair16_sum(hs);
+      hs = pair_sum(hs);
+      if ((lane & ~3) == 12) hpart[slot][wid][lane & 3] = hs;
+#else
       hs += __shfl_xor(hs, 4, 64);
       hs += __shfl_xor(hs, 8, 64);
       hs += __shfl_xor(hs, 16, 64);
       hs += __shfl_xor(hs, 32, 64);
       if (lane < 4) hpart[slot][wid][lane] = hs;
+#endif
     }
     if (lane == 0) {
       edge[slot][wid][0] = y.x;
@@ -297,13 +355,29 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     // lanes 0..3: block halo columns -2, -1, +0, +1
     const double yh = s.hx + A.alpha * (s.own ? hz : 0.0);
     const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WPB - 1) ? wid + 1 : WPB - 1;
+#if ARN_SELECT
+    // both candidates are read unconditionally (a uniform select, no branch around LDS reads)
+    const double el2 = edge[slot][wl][2], el1 = edge[slot][wl][3];
+    const double er1 = edge[slot][wr][0], er2 = edge[slot][wr][1];
+    const double hl2 = readlane(yh, 0), hl1 = readlane(yh, 1);
+    const double hr1 = readlane(yh, 2), hr2 = readlane(yh, 3);
+    const double yl2 = (wid == 0) ? hl2 : el2, yl1 = (wid == 0) ? hl1 : el1;
+    const double yr1 = (wid == WPB - 1) ? hr1 : er1, yr2 = (wid == WPB - 1) ? hr2 : er2;
+#else
     const double yl2 = (wid == 0) ? readlane(yh, 0) : edge[slot][wl][2];
     const double yl1 = (wid == 0) ? readlane(yh, 1) : edge[slot][wl][3];
     const double yr1 = (wid == WPB - 1) ? readlane(yh, 2) : edge[slot][wr][0];
     const double yr2 = (wid == WPB - 1) ? readlane(yh, 3) : edge[slot][wr][1];
-    // neighbours inside the half (width 32): lane l-1 holds columns 2l-2, 2l-1
+#endif
+    // neighbours inside the half: lane l-1 holds columns 2l-2, 2l-1 (the lanes whose neighbour
+    // is across the half boundary take the edge values below)
+#if ARN_DPPNB
+    const double ux = dpp_up(y.x), uy = dpp_up(y.y);
+    const double dx = dpp_down(y.x), dy = dpp_down(y.y);
+#else
     const double ux = __shfl_up(y.x, 1, 32), uy = __shfl_up(y.y, 1, 32);
     const double dx = __shfl_down(y.x, 1, 32), dy = __shfl_down(y.y, 1, 32);
+#endif
     const double cm2 = (l == 0) ? yl2 : ux, cm1 = (l == 0) ? yl1 : uy;   // columns 2l-2, 2l-1
     const double cp2 = (l == 31) ? yr1 : dx, cp3 = (l == 31) ? yr2 : dy;  // columns 2l+2, 2l+3
 #pragma unroll
@@ -344,7 +418,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
       const double Ly = applyL13(K, yc, a1, dg, a2);
       const double yy = yc * yc;
-      const double G = yc / K.k - (Ly + K.g * yy - yc * yy) / 2;
+      const double G = yc * K.ik - (Ly + K.g * yy - yc * yy) / 2;
       wo[q] = (G - g[q]) * isc;
     }
     const bool in = own && r < r1;
@@ -354,15 +428,16 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const dv2 wm = in ? wo : dv2{0.0, 0.0};
     const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
+    for (int k = 0; k < NB; ++k) {  // two chained FMAs per column pair
       const dv2 bi = d[k][lane];
-      aw[k] += wm.x * bi.x + wm.y * bi.y;
-      ag[k] += vm.x * bi.x + vm.y * bi.y;
+      aw[k] = __builtin_fma(wm.y, bi.y, __builtin_fma(wm.x, bi.x, aw[k]));
+      ag[k] = __builtin_fma(vm.y, bi.y, __builtin_fma(vm.x, bi.x, ag[k]));
     }
-    const double h0 = hf ? 0.0 : 1.0;  // the three squares once per column (half 0)
-    awn += h0 * (wm.x * vm.x + wm.y * vm.y);
-    avv += h0 * (vm.x * vm.x + vm.y * vm.y);
-    aww += h0 * (wm.x * wm.x + wm.y * wm.y);
+    // the three squares once per column (half 1 adds zeros)
+    const dv2 wh = hf ? dv2{0.0, 0.0} : wm, vh = hf ? dv2{0.0, 0.0} : vm;
+    awn = __builtin_fma(wh.y, vm.y, __builtin_fma(wh.x, vm.x, awn));
+    avv = __builtin_fma(vh.y, vm.y, __builtin_fma(vh.x, vm.x, avv));
+    aww = __builtin_fma(wh.y, wm.y, __builtin_fma(wh.x, wm.x, aww));
   };
   auto push_h2 = [&](const Slot& s, int64_t q) {
     const dv2 h2 = push(s, q);

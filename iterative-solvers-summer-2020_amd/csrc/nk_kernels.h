@@ -25,6 +25,7 @@ inline Field periodic(const double* p) { return Field{p, nullptr, nullptr}; }
 struct SHCoef {
   double c0, c1, c2, c3;  // centre, axial +-1, diagonal, axial +-2
   double k, g;            // time step, quadratic coefficient (sh_scipy_nk.py:18,29)
+  double ik;              // 1/k
 };
 SHCoef sh_coef(double h, double r, double k, double g);
 

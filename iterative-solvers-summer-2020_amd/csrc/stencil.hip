@@ -27,6 +27,7 @@ SHCoef sh_coef(double h, double r, double k, double g) {
   c.c2 = -2.0 * e * e;
   c.c3 = -e * e;
   c.k = k;
+  c.ik = 1.0 / k;
   c.g = g;
   return c;
 }
@@ -64,10 +65,12 @@ __device__ __forceinline__ double applyL(const SHCoef& k, const Nb& n) {
   return k.c0 * n.c + k.c1 * n.a1 + k.c2 * n.dg + k.c3 * n.a2;
 }
 
-// G(w) = w/k - (L w + g w^2 - w^3)/2, so that F(u) = G(u) + B(uo) (sh_scipy_nk.py:49).
+// G(w) = w/k - (L w + g w^2 - w^3)/2, so that F(u) = G(u) + B(uo) (sh_scipy_nk.py:49).  The
+// solver's kernels all scale by the host-rounded 1/k (no per-point division); the reference
+// residual (RESID) keeps the reference's (u - Uo)/k.
 __device__ __forceinline__ double Gfun(const SHCoef& k, double w, double Lw) {
   const double ww = w * w;
-  return w / k.k - (Lw + k.g * ww - w * ww) / 2;
+  return w * k.ik - (Lw + k.g * ww - w * ww) / 2;
 }
 
 template <SMode M>
@@ -87,20 +90,20 @@ __device__ __forceinline__ Res finish(const StencilArgs& A, const Nb& na, const 
   } else if constexpr (M == SMode::BOLD) {
     const double uo = na.c;
     const double uouo = uo * uo;
-    r.o0 = -uo / k.k - (applyL(k, na) + k.g * uouo - uo * uouo) / 2;
+    r.o0 = -uo * k.ik - (applyL(k, na) + k.g * uouo - uo * uouo) / 2;
   } else if constexpr (M == SMode::TRIAL) {
     const double G = Gfun(k, na.c, applyL(k, na));
     r.o0 = G + pv;
     r.o1 = G;
     r.o2 = na.c;
   } else if constexpr (M == SMode::FDJVP) {
-    r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) / sc;
+    r.o0 = (Gfun(k, na.c, applyL(k, na)) - pv) * sc;  // sc = 1/step here
   } else if constexpr (M == SMode::LINOP) {
     r.o0 = (1.0 + pv) * na.c - A.theta * applyL(k, na);
     r.o2 = na.c;
   } else {  // AJVP
     const double z = na.c, u = pv;
-    r.o0 = alpha * (z / k.k - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
+    r.o0 = alpha * (z * k.ik - (applyL(k, na) + (2.0 * k.g * u - 3.0 * u * u) * z) / 2);
   }
   return r;
 }
@@ -137,6 +140,7 @@ __device__ __forceinline__ void jvp_scale(const StencilArgs& A, double* alpha, d
       }
     }
   }
+  if constexpr (M == SMode::FDJVP) *sc = 1.0 / *sc;  // finish() scales by the reciprocal
 }
 
 // The point-wise input (G0, B, u or D) is streamed once per pass: optionally non-temporal, so it
