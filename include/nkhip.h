@@ -113,10 +113,12 @@ int nk_sh_fdjvp(const double* x0_dev, const double* G0_dev, const double* z_dev,
  * scipy/sparse/linalg/_isolve/_gcrotmk.py:104-143, plus the next KrylovJacobian.matvec,
  * scipy/optimize/_nonlin.py:1500-1513), in one pass over the basis:
  *   v = tau*w + sum_i coef[i]*V[i]                 -> v_out
- *   w' = (G(x0 + sc*zs*z) - G0)/sc,  z = v if z_dev == NULL   -> w_out
+ *   w' = (G(x0 + sc*zs*z) - G(x0))/sc,  z = v if z_dev == NULL   -> w_out
  *   dots[0..2nv+2] = [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']  (host; NULL: no reduction,
  *   no synchronisation).  nv <= 35, ny >= 8, nx >= 4 even, 16-B aligned vectors, periodic grid;
- *   v_out must not alias w or V[i]. */
+ *   v_out must not alias w or V[i].  The difference quotient is evaluated in closed form (G is a
+ *   cubic plus the linear 13-point stencil), equal to the two-evaluation quotient in exact
+ *   arithmetic but free of its cancellation, so G0_dev is not read (kept for the interface). */
 int nk_sh_arnoldi_fused(const double* const* V_dev, const double* coef, int32_t nv,
                         const double* w_dev, double tau, const double* x0_dev, const double* G0_dev,
                         const double* z_dev, int64_t ny, int64_t nx, double h, double r, double k,

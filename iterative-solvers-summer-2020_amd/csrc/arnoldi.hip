@@ -5,28 +5,30 @@
 // (KrylovJacobian.matvec, scipy/optimize/_nonlin.py:1500-1513 on the residual of
 // sh_scipy_nk.py:47-49):
 //   v      = tau*w + sum_i c_i V_i            (the Gram-Schmidt update of step j; c_i = -h_i sig_i)
-//   y      = x0 + alpha*z,  z = v (or an LGMRES augmentation vector when EXT)
-//   w'     = (G(y) - G0) / sc                 (the FD Jacobian-vector product of step j+1)
+//   u      = v (or an LGMRES augmentation vector z when EXT)
+//   w'     = (G(x0 + alpha u) - G(x0)) / sc   (the FD Jacobian-vector product of step j+1,
+//                                              evaluated in closed form, see centre())
 //   sums   w'.V_i, w'.v, v.V_i, v.v, w'.w'    (the multi-dot of step j+1, Gram row included)
 // so the basis V_0..V_j is read ONCE per Arnoldi step instead of twice (update + multi-dot), and
-// neither v nor w' is re-read.  Unfused, a step moves (2j + 9) vectors; fused (j + 6).
+// neither v nor w' is re-read.  Unfused, a step moves (2j + 9) vectors; fused (j + 5): V_0..V_j,
+// w and x0 in, v and w' out (the closed form needs no G0 = G(x0)).
 //
 // The stencil couples rows r-2..r+2, so a wave marches down a band of rows with the update running
 // two rows AHEAD of the stencil: at row r it forms v[r+2] from V_i[r+2], evaluates w'[r] on the
-// 5-row window of y, and takes the dot products of row r against V_i[r].  Loads run PF rows ahead
+// 5-row window of u, and takes the dot products of row r against V_i[r].  Loads run PF rows ahead
 // in a register ring (rotated by unrolling the walk by its length, so no register is copied); the
-// basis row and G0 of rows r, r+1 wait in an LDS ring for their dot products, which keeps the
+// basis row and x0 of rows r, r+1 wait in an LDS ring for their dot products, which keeps the
 // registers for loads in flight.  The basis length is a template parameter (fully unrolled).
 //
-// Lanes: one column per lane, 64 consecutive 512-B-aligned columns per wave (an aligned wave
-// segment streams at 62-68 % of peak in scripts/micro/pattern_bench.hip, an overlapping 60-column
-// one at 52-55 %).  The stencil's column halo (two columns each side) comes from PACKED halo loads:
-// in one instruction lane L fetches halo column L%4 of vector L/4 (16 vectors per instruction), a
-// 4-step xor-shuffle sums c_i V_i over the lanes of each column, and the four halo values of y are
-// read out to scalars.  Column neighbours inside the wave come from lane shuffles; no block
-// barrier.  Each band recomputes v on the two rows above and below it (band halo).  Per-lane sums
-// are wave-reduced once at the end and written as one partial per wave (deterministic: a fixed
-// wave -> rows mapping and a fixed order).
+// Lanes ("vector pairs", see arnoldi_kernel): a wave owns 64 aligned columns; one 16-B load per
+// lane streams two 512-B row segments of two entries (an aligned wave segment streams at 62-68 %
+// of peak in scripts/micro/pattern_bench.hip, an overlapping 60-column one at 52-55 %).  Column
+// neighbours inside the wave come from DPP lane shifts, the edge columns of the block's waves
+// through LDS (one barrier per row), and the block's outer halo (two columns each side) from
+// PACKED halo loads: lane L fetches halo column L%4 of entry L/4 (16 entries per instruction),
+// DPP/permlane sums form c_i V_i per column.  Each band recomputes v on the two rows above and
+// below it (band halo).  Per-lane sums are wave-reduced once at the end and written as one
+// partial per wave (deterministic: a fixed wave -> rows mapping and a fixed order).
 #include <cmath>
 #include <cstdlib>
 
@@ -149,7 +151,7 @@ __device__ __forceinline__ double dpp_down(double x) {
 
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
-//   [V_0 .. V_{NV-1}, w, x0, G0, (z)]
+//   [V_0 .. V_{NV-1}, w, x0, (z)]
 // in load k, so every load instruction streams two 512-B row segments of two vectors.  The update
 // sums each half's entries and adds the other half's sum (v_permlane32_swap); both halves then
 // hold v, y and w' of the wave's 64 columns, and each half takes the dot products of its own
@@ -157,13 +159,13 @@ __device__ __forceinline__ double dpp_down(double x) {
 template <int NV, bool EXT, int PF, bool NT>
 __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) {
   constexpr int RR = PF + 1;               // register ring: the update row and PF rows in flight
-  constexpr int NE = NV + 3 + (EXT ? 1 : 0);
+  constexpr int NE = NV + 2 + (EXT ? 1 : 0);
   constexpr int NI = (NE + 1) / 2;         // 16-B loads per row and lane
   constexpr int NB = (NV + 1) / 2;         // loads holding basis entries
-  constexpr int EX = NV + 1, EG = NV + 2, EZ = NV + 3;  // entries of x0, G0, z
-  // lag rows r, r+1 of this lane's basis entries and of G0, for row r's dot products / stencil
+  constexpr int EX = NV + 1, EZ = NV + 2;  // entries of x0, z
+  // lag rows r, r+1 of this lane's basis entries and of x0, for row r's dot products / stencil
   __shared__ dv2 lag[WPB][2][NB + 1][64];
-  // per row (parity slot): y on columns 0, 1, 62, 63 of every wave; the waves' partial sums of v
+  // per row (parity slot): u on columns 0, 1, 62, 63 of every wave; the waves' partial sums of v
   // on the block's four halo columns
   __shared__ double edge[2][WPB][4];
   __shared__ double hpart[2][WPB][4];
@@ -207,8 +209,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       if (e < NV) return A.V[e];
       if (e == NV) return A.w;
       if (e == EX) return A.x0;
-      if (e == EG) return A.g0;
-      return EXT ? A.z : A.g0;
+      return EXT ? A.z : A.x0;
     };
     auto cof = [&](int e) -> double { return e < NV ? A.c[e] : (e == NV ? A.tau : 0.0); };
     const int e0 = 2 * k, e1 = (2 * k + 1 < NE) ? 2 * k + 1 : 2 * k;
@@ -235,8 +236,8 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     hcf = cf;
   }
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
-  // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their y arrives in A.yh (the x0 entry
-  // and the x0 halo lanes read it there, and the row's update / z term is dropped)
+  // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their u arrives in A.yh (the x0 entry
+  // and the x0 halo lanes read it there in place of x0)
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
 
@@ -248,7 +249,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   struct Slot {
     dv2 e[NI];
     double hv, hx;
-    bool own;  // row of this slab (false: a neighbour's halo row, y taken from A.yh)
+    bool own;  // row of this slab (false: a neighbour's halo row, u taken from A.yh)
   };
   auto load = [&](Slot& s, int64_t q) {
     const int64_t qq = wrap(q);
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const bool mine = hf == (e & 1);
     return dv2{mine ? x.x : px, mine ? x.y : py};
   };
-  // the basis entries and G0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
+  // the basis entries and x0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
   auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
     dv2 (*d)[64] = lg[(q - r0) & 1];
 #pragma unroll
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   dv2 yw[5], hw[5], vw[5];
 #pragma unroll
   for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
-  dv2 gq{0.0, 0.0};  // G0 of the last pushed row (both halves)
+  dv2 gq{0.0, 0.0};  // x0 of the last pushed row (both halves)
   auto push = [&](const Slot& s, int64_t q) {
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
@@ -301,19 +302,19 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       p1 += ecf[k] * s.e[k].y;
     }
     const dv2 v{pair_sum(p0), pair_sum(p1)};
-    const dv2 x0 = both(s, EX);
-    gq = both(s, EG);
-    dv2 y;
+    // the stencil input u = v (or the augmentation vector z); on a slab's halo row the x0
+    // entry carries the neighbour's u
+    const dv2 xe = both(s, EX);
+    gq = xe;  // x0 of the row, for its centre step
+    dv2 u;
     if constexpr (EXT) {
-      const dv2 z0 = both(s, EZ);
-      const dv2 z = s.own ? z0 : dv2{0.0, 0.0};
-      y = dv2{x0.x + A.alpha * z.x, x0.y + A.alpha * z.y};
+      const dv2 z = both(s, EZ);
+      u = s.own ? z : xe;
     } else {
-      const dv2 u = s.own ? v : dv2{0.0, 0.0};
-      y = dv2{x0.x + A.alpha * u.x, x0.y + A.alpha * u.y};
+      u = s.own ? v : xe;
     }
     // block halo: this wave's share of c_i V_i on the four halo columns (sum over the 16 lanes
-    // of each column), exchanged with y on the edge columns of every wave through LDS
+    // of each column), exchanged with u on the edge columns of every wave through LDS
     const int slot = int(q & 1);
     if constexpr (!EXT) {
       // lane 4e + hh holds entry e (16 per instruction) of halo column hh: sum the four entries
@@ -335,12 +336,12 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 #endif
     }
     if (lane == 0) {
-      edge[slot][wid][0] = y.x;
-      edge[slot][wid][1] = y.y;
+      edge[slot][wid][0] = u.x;
+      edge[slot][wid][1] = u.y;
     }
     if (lane == 31) {
-      edge[slot][wid][2] = y.x;
-      edge[slot][wid][3] = y.y;
+      edge[slot][wid][2] = u.x;
+      edge[slot][wid][3] = u.y;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       for (int w = 0; w < WPB; ++w) hz += hpart[slot][w][hh];  // fixed order: deterministic
     }
     // lanes 0..3: block halo columns -2, -1, +0, +1
-    const double yh = s.hx + A.alpha * (s.own ? hz : 0.0);
+    const double yh = s.own ? hz : s.hx;  // u on the halo columns
     const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WPB - 1) ? wid + 1 : WPB - 1;
 #if ARN_SELECT
     // both candidates are read unconditionally (a uniform select, no branch around LDS reads)
@@ -372,11 +373,11 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     // neighbours inside the half: lane l-1 holds columns 2l-2, 2l-1 (the lanes whose neighbour
     // is across the half boundary take the edge values below)
 #if ARN_DPPNB
-    const double ux = dpp_up(y.x), uy = dpp_up(y.y);
-    const double dx = dpp_down(y.x), dy = dpp_down(y.y);
+    const double ux = dpp_up(u.x), uy = dpp_up(u.y);
+    const double dx = dpp_down(u.x), dy = dpp_down(u.y);
 #else
-    const double ux = __shfl_up(y.x, 1, 32), uy = __shfl_up(y.y, 1, 32);
-    const double dx = __shfl_down(y.x, 1, 32), dy = __shfl_down(y.y, 1, 32);
+    const double ux = __shfl_up(u.x, 1, 32), uy = __shfl_up(u.y, 1, 32);
+    const double dx = __shfl_down(u.x, 1, 32), dy = __shfl_down(u.y, 1, 32);
 #endif
     const double cm2 = (l == 0) ? yl2 : ux, cm1 = (l == 0) ? yl1 : uy;   // columns 2l-2, 2l-1
     const double cp2 = (l == 31) ? yr1 : dx, cp3 = (l == 31) ? yr2 : dy;  // columns 2l+2, 2l+3
@@ -386,10 +387,10 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       hw[m] = hw[m + 1];
       vw[m] = vw[m + 1];
     }
-    yw[4] = y;
-    hw[4] = dv2{cm1 + y.y, y.x + cp2};
+    yw[4] = u;
+    hw[4] = dv2{cm1 + u.y, u.x + cp2};
     vw[4] = v;
-    // the h2 = y[c-2] + y[c+2] of row q is needed only when q is the window centre: keep the
+    // the h2 = u[c-2] + u[c+2] of row q is needed only when q is the window centre: keep the
     // four outer neighbours of the row two steps back
     const bool st = own && hf == 0 && q >= r0 && q < r1;
     const __amdgpu_buffer_rsrc_t r = rv;
@@ -405,21 +406,27 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   dv2 h2w[3];  // h2 of rows r, r+1, r+2
 #pragma unroll
   for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
-  // stencil + dot products of row r (window centre = row r; basis row r and G0 from LDS)
+  // stencil + dot products of row r (window centre = row r; basis row r and x0 from LDS).
+  // w' = (G(x0 + a u) - G(x0)) / sc in closed form: G is a cubic in its argument plus the linear
+  // stencil, so the difference quotient is exactly
+  //   (a/sc) [u/k - (L u + u (g (2 x0 + t) - (3 x0 (x0 + t) + t^2)))/2],  t = a u,
+  // without the cancellation of two G evaluations (and without reading G0).
+  const double zs = A.alpha * isc;
   auto centre = [&](int64_t r) {
     const dv2 (*d)[64] = lg[(r - r0) & 1];
-    const dv2 g = d[NB][lane];
+    const dv2 x0r = d[NB][lane];
     dv2 wo;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const double yc = yw[2][q];
+      const double uc = yw[2][q];
       const double a1 = hw[2][q] + (yw[1][q] + yw[3][q]);
       const double dg = hw[1][q] + hw[3][q];
       const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
-      const double Ly = applyL13(K, yc, a1, dg, a2);
-      const double yy = yc * yc;
-      const double G = yc * K.ik - (Ly + K.g * yy - yc * yy) / 2;
-      wo[q] = (G - g[q]) * isc;
+      const double Lu = applyL13(K, uc, a1, dg, a2);
+      const double x = x0r[q];
+      const double t = A.alpha * uc;
+      const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
+      wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
@@ -589,8 +596,8 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   }
 }
 
-// y on the edge rows 0, 1, ny-2, ny-1 of a slab (grid: column blocks x 4 rows).  The update sum
-// runs in the fused kernel's order -- entries 0, 2, 4, .. of [V_0 .. V_{nv-1}, w] in one partial,
+// u (= v, or z) on the edge rows 0, 1, ny-2, ny-1 of a slab (grid: column blocks x 4 rows).
+// The update sum runs in the fused kernel's order -- entries 0, 2, 4, .. of [V_0 .. V_{nv-1}, w] in one partial,
 // 1, 3, 5, .. in the other, then their sum -- so a halo row equals the row its owner computes.
 __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4) {
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -598,9 +605,9 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
   const int t = blockIdx.y;
   const int64_t row = (t < 2) ? t : A.ny - 4 + t;
   const int64_t o = row * A.nx + j;
-  double y;
+  double y;  // the stencil input u of the fused kernel
   if (A.z) {
-    y = A.x0[o] + A.alpha * A.z[o];
+    y = A.z[o];
   } else {
     double p[2] = {0.0, 0.0};
     for (int e = 0; e <= A.nv; ++e) {
@@ -608,8 +615,7 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
       const double c = (e < A.nv) ? A.c[e] : A.tau;
       p[e & 1] += c * x;
     }
-    const double v = p[0] + p[1];
-    y = A.x0[o] + A.alpha * v;
+    y = p[0] + p[1];
   }
   y4[int64_t(t) * A.nx + j] = y;
 }
@@ -632,7 +638,7 @@ bool arnoldi_supported(int nv, int64_t ny, int64_t nx) {
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   if (!arnoldi_supported(A.nv, A.ny, A.nx)) return hipErrorInvalidValue;
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
-  bool al = al16(A.w) && al16(A.x0) && al16(A.g0) && al16(A.z) && al16(A.out_v) && al16(A.out_w);
+  bool al = al16(A.w) && al16(A.x0) && al16(A.z) && al16(A.out_v) && al16(A.out_w);
   for (int i = 0; i < A.nv; ++i) al = al && al16(A.V[i]);
   if (!al) return hipErrorInvalidValue;  // 16-B loads and stores
   if (A.z) return launch_e<true>(A, s, nwaves);

@@ -155,7 +155,8 @@ int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, 
                         double tau, const double* x0, const double* G0, const double* z,
                         int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
                         double sc, double* v_out, double* w_out, double* dots, void* stream) {
-  if (!V || !coef || !w || !x0 || !G0 || !v_out || !w_out || !(sc != 0.0)) return NK_EINVAL;
+  // G0 is not read (closed-form difference quotient) and may be NULL
+  if (!V || !coef || !w || !x0 || !v_out || !w_out || !(sc != 0.0)) return NK_EINVAL;
   if (!arnoldi_supported(nv, ny, nx)) return NK_EINVAL;
   ArnoldiArgs A;
   A.ny = ny;

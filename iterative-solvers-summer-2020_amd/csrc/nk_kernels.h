@@ -127,14 +127,14 @@ struct ArnoldiArgs {
   const double* w = nullptr;       // previous JVP output
   double tau = 1.0;
   const double* x0 = nullptr;      // Newton iterate
-  const double* g0 = nullptr;      // G(x0)
+  const double* g0 = nullptr;      // G(x0): not read (the JVP is evaluated in closed form)
   const double* z = nullptr;       // JVP input if not the new v (LGMRES augmentation vector)
-  double alpha = 0.0;              // y = x0 + alpha z
-  double sc = 1.0;                 // w' = (G(y) - G0)/sc
+  double alpha = 0.0;              // w' = (G(x0 + alpha u) - G(x0))/sc with u = v or z
+  double sc = 1.0;
   SHCoef k{};
   double* out_v = nullptr;         // must not alias w or any V_i
   double* out_w = nullptr;
-  // row slab (one of several): y on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
+  // row slab (one of several): u on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
   // arnoldi_edge_launch on every rank + the halo exchange); nullptr = single periodic slab
   const double* yh = nullptr;
   double* partial = nullptr;       // [(2 nv + 3)][nwaves]
@@ -143,7 +143,7 @@ struct ArnoldiArgs {
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
-// y = x0 + alpha v (or alpha z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
+// u = v (or z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
 // with the fused kernel's summation order: what the neighbours need as their halo rows
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
 

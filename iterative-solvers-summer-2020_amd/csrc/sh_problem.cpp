@@ -213,8 +213,8 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   return halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
 }
 
-// One launch per Arnoldi step with the FD JVP (arnoldi.hip).  On a row slab the kernel needs y
-// on the neighbours' two edge rows: every rank first evaluates y on its own edge rows (a 4-row
+// One launch per Arnoldi step with the FD JVP (arnoldi.hip).  On a row slab the kernel needs u
+// on the neighbours' two edge rows: every rank first evaluates u on its own edge rows (a 4-row
 // launch), exchanges them, then runs the fused pass with those rows as its halo.
 // NKHIP_FUSED=0 disables it (read per call, so a test can compare both paths in one process).
 bool SHProblem::has_fused(int nv) const {
@@ -249,8 +249,8 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   A.partial = E_.partial();
   A.partial_cap = E_.partial_cap();
   if (dist()) {
-    // edge rows of y -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
-    const double eb = 8.0 * 4 * nx_ * (z ? 3 : nv + 3);
+    // edge rows of u -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
+    const double eb = 8.0 * 4 * nx_ * (z ? 2 : nv + 2);
     int rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
     if (rc) return rc;
     rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
@@ -260,8 +260,8 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     if (rc) return NK_ECOMM;
     A.yh = yh_;
   }
-  // algorithmic bytes: read V (nv), w, x0, G0 (, z); write v, w'
-  const double bytes = 8.0 * double(ny_ * nx_) * (nv + 5 + (z ? 1 : 0));
+  // algorithmic bytes: read V (nv), w, x0 (, z); write v, w'
+  const double bytes = 8.0 * double(ny_ * nx_) * (nv + 4 + (z ? 1 : 0));
   return E_.launch(K_ARNOLDI, bytes, [&] { return arnoldi_launch(A, E_.s, nwaves); });
 }
 

@@ -48,7 +48,7 @@ class SHProblem final : public Problem {
   double* hz_ = nullptr;
   double* hd_ = nullptr;
   double* hu_ = nullptr;
-  double* y4_ = nullptr;  // fused Arnoldi step: y on this slab's edge rows 0, 1, ny-2, ny-1
+  double* y4_ = nullptr;  // fused Arnoldi step: u on this slab's edge rows 0, 1, ny-2, ny-1
   double* yh_ = nullptr;  // ... and on the halo rows -2, -1, ny, ny+1 from the neighbours
   int64_t ny_min_ = 0, ny_max_ = 0;  // smallest / largest slab over the ranks
   hipStream_t side_ = nullptr;       // interior rows of the JVP while the halo is in flight

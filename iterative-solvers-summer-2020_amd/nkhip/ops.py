@@ -100,10 +100,11 @@ def sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=None, ny=Non
                      v_out=None, w_out=None, reduce=True):
     """One fused Arnoldi step (csrc/arnoldi.hip): the Gram-Schmidt update of scipy's _fgmres
     (_gcrotmk.py:104-143) ``v = tau*w + sum_i coef[i]*V[i]``, the next FD matvec
-    (_nonlin.py:1500-1513) ``w' = (G(x0 + sc*zs*z) - G0)/sc`` with ``z = v`` unless given, and the
-    next multi-dot, all in one pass over the basis.  Returns ``(v, w', dots)`` with
-    ``dots = [w'.V_i..., w'.v, v.V_i..., v.v, w'.w']`` (None when ``reduce`` is False)."""
-    for t, nm in ((w, "w"), (x0, "x0"), (G0, "G0")):
+    (_nonlin.py:1500-1513) ``w' = (G(x0 + sc*zs*z) - G(x0))/sc`` with ``z = v`` unless given, and
+    the next multi-dot, all in one pass over the basis.  Returns ``(v, w', dots)`` with
+    ``dots = [w'.V_i..., w'.v, v.V_i..., v.v, w'.w']`` (None when ``reduce`` is False).  The
+    difference quotient is evaluated in closed form, so ``G0`` is not read (it may be None)."""
+    for t, nm in ((w, "w"), (x0, "x0")):
         _dev(t, nm)
     ny, nx = _grid(x0, ny, nx)
     nv = len(V)
@@ -113,7 +114,8 @@ def sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=None, ny=Non
     w_out = torch.empty_like(x0) if w_out is None else _dev(w_out, "w_out")
     dots = (C.c_double * (2 * nv + 3))() if reduce else None
     zp = _ptr(_dev(z, "z")) if z is not None else None
-    check(lib.nk_sh_arnoldi_fused(ptrs, cf, nv, _ptr(w), float(tau), _ptr(x0), _ptr(G0), zp, ny,
+    check(lib.nk_sh_arnoldi_fused(ptrs, cf, nv, _ptr(w), float(tau), _ptr(x0),
+                                  _ptr(G0) if G0 is not None else None, zp, ny,
                                   nx, float(h), float(r), float(k), float(g), float(zs),
                                   float(sc), _ptr(v_out), _ptr(w_out), dots, _stream()),
           "nk_sh_arnoldi_fused")

@@ -8,5 +8,5 @@ for v in "$@"; do
   [ "$v" = A ] && lib=$PWD/iterative-solvers-summer-2020_amd/nkhip/libnkhip.so
   echo "== $v"
   NKHIP_LIB=$lib timeout -k 10 120 python -u scripts/arnoldi_bench.py > gpurun_out/arnv_$v.log 2>&1 || exit $?
-  grep -v amdgpu.ids gpurun_out/arnv_$v.log | python3 -c "import sys,json; r=[json.loads(l) for l in sys.stdin]; print(' '.join(('E' if x['ext'] else 'n')+str(x['nv'])+':'+str(int(x['GBps'])) for x in r))"
+  grep -v amdgpu.ids gpurun_out/arnv_$v.log | python3 -c "import sys,json; r=[json.loads(l) for l in sys.stdin]; print(' '.join(('E' if x['ext'] else 'n')+str(x['nv'])+':'+str(int(x['us'])) for x in r))"
 done

@@ -1,7 +1,7 @@
 """Microbenchmark of the fused Arnoldi step (csrc/arnoldi.hip) at 4096^2 over the basis length.
 
 Prints one line per (nv, ext): average kernel time (HIP events around 20 launches, no reduction)
-and the algorithmic rate 8 n (nv + 5 + ext) bytes / time against the 8 TB/s HBM peak.  Tuning
+and the algorithmic rate 8 n (nv + 4 + ext) bytes / time against the 8 TB/s HBM peak.  Tuning
 knobs are environment variables read once per process (NKHIP_ARN_PF, NKHIP_ARN_NT,
 NKHIP_ARN_ROUNDS), so compare configurations in separate processes.
 """
@@ -41,7 +41,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             us = a.elapsed_time(b) * 1e3 / reps
-            byt = 8.0 * n * (nv + 5 + (1 if ext else 0))
+            byt = 8.0 * n * (nv + 4 + (1 if ext else 0))
             out.append({"nv": nv, "ext": ext, "us": round(us, 2),
                         "GBps": round(byt / us / 1e3, 1), "frac": round(byt / us / 1e3 / 8000, 3)})
             print(json.dumps(out[-1]), flush=True)
