@@ -71,18 +71,38 @@ def main():
                                        if k in bench}, indent=1), "```"]
     open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w").write("\n".join(out) + "\n")
     print("\n".join(out))
-    # per-kernel-class HBM traffic per launch (PMC) next to the algorithmic bytes of the SAME run
-    classes = {"combo_kernel<true>": "krylov_combo", "mdot_kernel<true>": "krylov_mdot",
-               "combo_kernel<true, true>": "krylov_combo", "mdot_kernel<true, true>": "krylov_mdot",
-               "march_kernel<(nk::SMode)5, 128>": "sh_fdjvp",
-               "march_kernel<(nk::SMode)6, 128>": "sh_ajvp",
-               "march_kernel<(nk::SMode)4, 128>": "sh_trial",
-               "march_kernel<(nk::SMode)3, 128>": "sh_bold",
-               "reduce_final_kernel": "reduce_final"}
+    # per-kernel-class HBM traffic per launch (PMC) next to the algorithmic bytes of the SAME run;
+    # a class sums every instantiation of its kernel template (arnoldi_kernel<nv, ext, pf, nt>)
+    def klass(k):
+        if k.startswith("arnoldi_kernel<"):
+            return "arnoldi_fused"
+        if k.startswith("arnoldi_edge_kernel"):
+            return "arnoldi_edge"
+        if k.startswith("combo_kernel<"):
+            return "krylov_combo"
+        if k.startswith("mdot_kernel<"):
+            return "krylov_mdot"
+        if k.startswith("reduce_final_kernel"):
+            return "reduce_final"
+        for mode, cls in (("5", "sh_fdjvp"), ("6", "sh_ajvp"), ("4", "sh_trial"), ("3", "sh_bold")):
+            if k.startswith(f"march_kernel<(nk::SMode){mode},"):
+                return cls
+        return None
+
+    def by_class(agg):
+        out = collections.defaultdict(lambda: [0, 0.0])
+        for k, (n, v) in agg.items():
+            c = klass(k)
+            if c:
+                out[c][0] += n
+                out[c][1] += v
+        return out
+
+    fc, wc = by_class(fetch), by_class(write)
     traffic = {"tag": tag, "source": f"profiles/{tag}_summary.md", "classes": {}}
-    for k, cls in classes.items():
-        f, w = fetch.get(k), write.get(k)
-        if not f or not w or not f[0]:
+    for cls in sorted(fc):
+        f, w = fc[cls], wc.get(cls)
+        if not w or not f[0] or not w[0]:
             continue
         rec = {"launches": f[0], "hbm_read_bytes_per_launch": 2 * f[1] * 1024 / f[0],
                "hbm_write_bytes_per_launch": w[1] * 1024 / w[0]}
