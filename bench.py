@@ -240,6 +240,39 @@ def config_droplet_init():
                                     "container; tests/test_oracle_droplet.py)"}
 
 
+def jvp_isolated(n, h, r, k, g, x0, jvp, reps=20):
+    """The JVP stencil the metric names, alone: `reps` back-to-back launches on resident n^2
+    inputs (after the timed region), HIP events on the launch stream.  FD: reads x0, z, G0 and
+    writes w (32 B/pt); analytic: reads u, z, writes Jz (24 B/pt)."""
+    import torch
+
+    import nkhip
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    z = torch.randn(n, n, dtype=torch.float64, device="cuda", generator=gen)
+    g0 = torch.randn(n, n, dtype=torch.float64, device="cuda", generator=gen)
+    w = torch.empty_like(z)
+    x = x0.reshape(n, n)
+    if jvp == "fd":
+        fn, bpp, name = (lambda: nkhip.sh_fdjvp(x, g0, z, h, r, k, g, 1.0, 1e-7, out=w)), 32, "sh_fdjvp"
+    else:
+        fn, bpp, name = (lambda: nkhip.sh_jvp(x, z, h, r, k, g, out=w)), 24, "sh_ajvp"
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / reps
+    gbs = bpp * n * n / (us * 1e-6) / 1e9
+    return {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_us": round(us, 2),
+            "alg_bytes_per_launch": bpp * n * n, "launches": reps,
+            "source": f"{reps} back-to-back launches on resident {n}^2 inputs after the timed region"}
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "latest_traffic.json")
     try:
@@ -375,6 +408,8 @@ def main():
             "state_max_abs": final_max,
             "cpu_baseline": None,
         }
+        if world == 1:
+            out["jvp_roofline_isolated"] = jvp_isolated(n, h, r, k, g, a, args.jvp)
         if world == 1 and args.cpu_baseline == "auto":
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
             out["cpu_baseline"] = cpu_baseline(n, h, k, r, g, fe)

@@ -41,10 +41,10 @@ def lap5(v: np.ndarray, ny: int, nx: int, e: float) -> np.ndarray:
     return out.reshape(-1)
 
 
-def sh13(v: np.ndarray, ny: int, nx: int, h: float, r: float) -> np.ndarray:
+def sh13(v: np.ndarray, ny: int, nx: int, h: float, r: float, dtype=np.float64) -> np.ndarray:
     """``L @ v`` with L = -Lap^2 - 2 Lap + (r-1) I (sh_scipy_nk.py:38-39), matrix-free."""
-    c0, c1, c2, c3 = sh_coeffs(h, r)
-    v2 = np.asarray(v, dtype=np.float64).reshape(ny, nx)
+    c0, c1, c2, c3 = (dtype(c) for c in sh_coeffs(h, r))
+    v2 = np.asarray(v, dtype=dtype).reshape(ny, nx)
     ax1 = _sh(v2, 1, 0) + _sh(v2, -1, 0) + _sh(v2, 0, 1) + _sh(v2, 0, -1)
     dg = _sh(v2, 1, 1) + _sh(v2, 1, -1) + _sh(v2, -1, 1) + _sh(v2, -1, -1)
     ax2 = _sh(v2, 2, 0) + _sh(v2, -2, 0) + _sh(v2, 0, 2) + _sh(v2, 0, -2)
@@ -63,6 +63,30 @@ def residual(u, uo, ny, nx, h, r, k, g):
 def jvp(u, v, ny, nx, h, r, k, g):
     """Exact Jacobian-vector product of ``residual`` at u: v/k - (Lv + (2g u - 3u^2) v)/2."""
     return v / k - (sh13(v, ny, nx, h, r) + (2.0 * g * u - 3.0 * u * u) * v) / 2
+
+
+def fd_quotient(x0, u, alpha, sc, ny, nx, h, r, k, g, dtype=np.float64):
+    """KrylovJacobian.matvec's difference quotient (_nonlin.py:1505-1509) on this residual,
+    (F(x0 + alpha u) - F(x0)) / sc, evaluated with two residual evaluations (as SciPy does) in
+    ``dtype``; F's constant part (the Uo terms) cancels, so G(w) = w/k - (Lw + g w^2 - w^3)/2."""
+    x0 = np.asarray(x0, dtype=dtype)
+    y = x0 + dtype(alpha) * np.asarray(u, dtype=dtype)
+
+    def G(w):
+        return w / dtype(k) - (sh13(w, ny, nx, h, r, dtype) + dtype(g) * w * w - w * w * w) / 2
+
+    return (G(y) - G(x0)) / dtype(sc)
+
+
+def fd_quotient_closed_form(x0, u, alpha, sc, ny, nx, h, r, k, g):
+    """The same quotient in closed form (the fused Arnoldi kernel, csrc/arnoldi.hip): G is a
+    cubic in w plus the linear stencil, so exactly
+    (alpha/sc) [u/k - (L u + u (g (2 x0 + t) - (3 x0 (x0 + t) + t^2)))/2],  t = alpha u."""
+    x0 = np.asarray(x0, dtype=np.float64)
+    u = np.asarray(u, dtype=np.float64)
+    t = alpha * u
+    D = g * (2.0 * x0 + t) - (3.0 * x0 * (x0 + t) + t * t)
+    return (alpha / sc) * (u / k - (sh13(u, ny, nx, h, r) + u * D) / 2)
 
 
 # --------------------------------------------------------------------------------------

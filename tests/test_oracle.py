@@ -84,3 +84,29 @@ def test_nk_restatement_raises_like_scipy():
     F = lambda u: sh_oracle.residual(u, uo, N, N, h, 0.01, 0.2, 1.0)  # noqa: E731
     with pytest.raises(nk_oracle.NoConvergence):
         nk_oracle.newton_krylov(F, uo, maxiter=1)
+
+
+@pytest.mark.parametrize("alpha", [1e-8, 1e-4, 0.3])
+def test_fd_quotient_closed_form(alpha):
+    """The fused kernel's closed-form JVP equals SciPy's two-evaluation difference quotient: exactly
+    in exact arithmetic, so against the quotient evaluated in extended precision it agrees to
+    double rounding, while the float64 two-evaluation form carries its cancellation error
+    ~eps |G| / (alpha |J u|) (largest at SciPy's tiny steps)."""
+    N, h, r, k, g = 48, 0.625, 0.01, 0.2, 1.0
+    rng = np.random.default_rng(5)
+    x0 = rng.standard_normal(N * N)
+    u = rng.standard_normal(N * N) / N
+    sc = alpha / 0.5
+    closed = sh_oracle.fd_quotient_closed_form(x0, u, alpha, sc, N, N, h, r, k, g)
+    ext = sh_oracle.fd_quotient(x0, u, alpha, sc, N, N, h, r, k, g, dtype=np.longdouble)
+    two = sh_oracle.fd_quotient(x0, u, alpha, sc, N, N, h, r, k, g)
+    scale = float(np.abs(ext).max())
+    err_closed = float(np.abs(closed - ext.astype(np.float64)).max()) / scale
+    err_two = float(np.abs(two - ext.astype(np.float64)).max()) / scale
+    # long double has 64-bit mantissa here; its own error is ~eps_ld |G| / (alpha |J u|)
+    eps_ld = float(np.finfo(np.longdouble).eps)
+    assert err_closed <= 1e-13 + 1e3 * eps_ld / alpha
+    assert err_closed <= err_two + 1e-13
+    # the two-evaluation form's error grows as the step shrinks; the closed form's does not
+    if alpha <= 1e-4:
+        assert err_two >= 10 * err_closed
