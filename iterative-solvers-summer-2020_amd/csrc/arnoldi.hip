@@ -591,8 +591,16 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   if constexpr (NV > kArnMaxNV) {
     return hipErrorInvalidValue;
   } else {
+#ifdef ARN_NV_ONLY  // ISA inspection builds: instantiate one basis length only
+    if constexpr (NV != ARN_NV_ONLY) {
+      return launch_e<EXT, NV + 1>(A, s, nwaves);
+    } else {
+      return launch_pf<NV, EXT>(A, s, nwaves);
+    }
+#else
     if (A.nv == NV) return launch_pf<NV, EXT>(A, s, nwaves);
     return launch_e<EXT, NV + 1>(A, s, nwaves);
+#endif
   }
 }
 
