@@ -119,7 +119,8 @@ def test_fused_kernel_vs_torch(ny, nx, nv, ext):
         assert abs(a - b) <= 1e-10 * scale, (i, a, b)
 
 
-@pytest.mark.parametrize("nranks,ny_total,nx", [(2, 64, 64), (3, 96, 130), (4, 48, 40)])
+@pytest.mark.parametrize("nranks,ny_total,nx", [(2, 64, 64), (3, 96, 130), (4, 48, 40),
+                                                  (8, 1024, 1024)])
 def test_fused_slabs_match_single_slab(nranks, ny_total, nx):
     """Row slabs through the fused kernel: every rank evaluates y on its edge rows, the loopback
     communicator exchanges them (the RCCL path's protocol), and the fused pass takes them as its
