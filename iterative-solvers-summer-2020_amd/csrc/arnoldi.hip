@@ -617,13 +617,31 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
   if (A.z) {
     y = A.z[o];
   } else {
-    double p[2] = {0.0, 0.0};
-    for (int e = 0; e <= A.nv; ++e) {
-      const double x = (e < A.nv) ? A.V[e][o] : A.w[o];
-      const double c = (e < A.nv) ? A.c[e] : A.tau;
-      p[e & 1] += c * x;
+    // entries [V_0 .. V_{nv-1}, w] in batches of 8 loads in flight (the kernel is latency-bound:
+    // 4 rows of a slab); the sums stay in entry order within each parity
+    const int ne = A.nv + 1;
+    auto ent = [&](int e) -> const double* { return (e < A.nv) ? A.V[e] : A.w; };
+    auto cof = [&](int e) -> double { return (e < A.nv) ? A.c[e] : A.tau; };
+    double p0 = 0.0, p1 = 0.0;
+    int e = 0;
+    for (; e + 8 <= ne; e += 8) {
+      double x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = ent(e + q)[o];
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        p0 += cof(e + q) * x[q];
+        p1 += cof(e + q + 1) * x[q + 1];
+      }
     }
-    y = p[0] + p[1];
+    for (; e < ne; ++e) {
+      const double x = ent(e)[o];
+      if (e & 1)
+        p1 += cof(e) * x;
+      else
+        p0 += cof(e) * x;
+    }
+    y = p0 + p1;
   }
   y4[int64_t(t) * A.nx + j] = y;
 }
