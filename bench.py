@@ -46,43 +46,52 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, h, k, r, g, fevals_per_step):
-    """The reference's CPU path (scipy CSR L + scipy.optimize.newton_krylov, oracle/sh_oracle.py),
-    timed on a bounded sample: the FIRST Newton iteration of step 0 at the full grid size."""
+def cpu_baseline(n, h, k, r, g, u_start, gpu_fevals_per_step):
+    """The reference's CPU path (scipy CSR L + scipy.optimize.newton_krylov on the reference
+    residual, oracle/sh_oracle.py) timed on ONE full implicit step at the full grid size, from
+    the same state the GPU's first timed step started from (so the same step of the trajectory).
+    The first Newton iteration's time, extrapolated with the GPU run's F evals per step, is
+    reported beside it (round-1 method).  Returns (record, the CPU's next state)."""
     import numpy as np
-    from scipy.optimize import NoConvergence, newton_krylov
+    from scipy.optimize import newton_krylov
 
     from oracle import sh_oracle
 
     L = sh_oracle.csr_L(n, h, r)
-    U0 = np.random.default_rng(2020).standard_normal(n * n)
     cnt = [0]
-    f = sh_oracle.make_csr_residual(L, U0, k, g, cnt)
+    f = sh_oracle.make_csr_residual(L, u_start, k, g, cnt)
+    marks = []
     t0 = time.perf_counter()
-    try:
-        newton_krylov(f, U0, maxiter=1)
-    except NoConvergence:
-        pass
+    u_next = newton_krylov(f, u_start, callback=lambda x, fx: marks.append(
+        (time.perf_counter() - t0, cnt[0])))
     dt = time.perf_counter() - t0
-    s_per_feval = dt / max(cnt[0], 1)
-    step_s = s_per_feval * fevals_per_step
+    t1, f1 = marks[0] if marks else (dt, cnt[0])
     try:
         import threadpoolctl
         blas_threads = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
     except Exception:
         blas_threads = os.cpu_count() or 1
-    return {
-        "value": 1.0 / step_s,
+    rec = {
+        "value": 1.0 / dt,
         "unit": "steps/s",
         "cores": int(blas_threads),
         "kind": "port",
-        "sample": (f"scipy CSR L ({L.nnz} nnz) + scipy.optimize.newton_krylov: first Newton "
-                   f"iteration of step 0 at {n}^2 ({cnt[0]} F evals incl. FD-JVPs, {dt:.1f} s, "
-                   f"{s_per_feval:.3f} s/F-eval incl. its LGMRES work); steps/s extrapolated with "
-                   f"the {fevals_per_step:.0f} F evals/step the GPU run needed (same algorithm). "
-                   f"csr_matvec and NumPy element-wise are single-threaded; OpenBLAS BLAS-1 uses "
-                   f"{blas_threads} threads; os.cpu_count()={os.cpu_count()}"),
+        "sample": (f"ONE full implicit step at {n}^2 timed (scipy CSR L, {L.nnz} nnz, + "
+                   f"scipy.optimize.newton_krylov on the reference residual): {dt:.1f} s, "
+                   f"{len(marks)} Newton its, {cnt[0]} F evals, from the state the GPU's first "
+                   f"timed step started from. csr_matvec and NumPy element-wise are "
+                   f"single-threaded; OpenBLAS BLAS-1 uses {blas_threads} threads; "
+                   f"os.cpu_count()={os.cpu_count()}"),
+        "step_s": round(dt, 2),
+        "newton_its": len(marks),
+        "fevals": cnt[0],
+        "first_iteration_extrapolated": {
+            "value": 1.0 / (t1 / max(f1, 1) * gpu_fevals_per_step),
+            "first_iteration_s": round(t1, 2), "first_iteration_fevals": f1,
+            "method": "s per F eval of the first Newton iteration x the GPU run's F evals per "
+                      "step (round-1 estimate)"},
     }
+    return rec, u_next
 
 
 def config2_lap5(n=1024, reps=200):
@@ -326,6 +335,8 @@ def main():
     for _ in range(args.warmup):
         model.step(a, out=b)
         a, b = b, a
+    want_cpu = world == 1 and args.cpu_baseline == "auto"
+    u_start = a.cpu().numpy().reshape(-1) if want_cpu else None  # outside the timed region
     model.reset_profile()
     tot = {"nit": 0, "nfev": 0, "njvp": 0, "n_arnoldi": 0}
     barrier()
@@ -343,6 +354,19 @@ def main():
         elapsed = float(t.item())
     prof = model.kernel_profile()
     final_max = float(a.abs().max())
+    # check the final step on the host (outside the timed region): a = U[s+1], b = U[s]; with
+    # N > 1 the slabs are gathered to every rank and rank 0 evaluates the oracle residual
+    # (sh_scipy_nk.py:47-49) of the whole grid
+    if world > 1:
+        ga = [torch.empty_like(a) for _ in range(world)]
+        gb = [torch.empty_like(b) for _ in range(world)]
+        dist.all_gather(ga, a.contiguous())
+        dist.all_gather(gb, b.contiguous())
+        full_a = torch.cat(ga).cpu().numpy() if rank == 0 else None
+        full_b = torch.cat(gb).cpu().numpy() if rank == 0 else None
+        del ga, gb
+    else:
+        full_a, full_b = a.cpu().numpy(), b.cpu().numpy()
 
     if rank == 0:
         steps_per_s = args.steps / elapsed
@@ -372,6 +396,13 @@ def main():
                     "alg_bytes_per_launch": alg,
                     "traffic_source": traffic_db.get("source") if traffic else None}
 
+        from oracle import sh_oracle
+        F_last = sh_oracle.residual(full_a.reshape(-1), full_b.reshape(-1), n, n, h, r, k, g)
+        final_check = {"max_abs_residual": float(np.abs(F_last).max()),
+                       "f_tol": float(np.finfo(float).eps ** (1 / 3)),
+                       "what": "oracle residual (sh_scipy_nk.py:47-49) of the last timed step, "
+                               "evaluated on the host over the whole grid"}
+        del F_last
         jvp_name = "sh_fdjvp" if args.jvp == "fd" else "sh_ajvp"
         kernel_ms = sum(v["ms_est"] for v in ker.values())
         out = {
@@ -406,13 +437,24 @@ def main():
                         for k_, v in ker.items()},
             "kernel_timing": f"HIP events around every {profile}-th launch of each class",
             "state_max_abs": final_max,
+            "final_step_check": final_check,
             "cpu_baseline": None,
         }
         if world == 1:
             out["jvp_roofline_isolated"] = jvp_isolated(n, h, r, k, g, a, args.jvp)
-        if world == 1 and args.cpu_baseline == "auto":
+        if want_cpu:
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
-            out["cpu_baseline"] = cpu_baseline(n, h, k, r, g, fe)
+            rec, u_cpu = cpu_baseline(n, h, k, r, g, u_start, fe)
+            # the same step on the GPU (outside the timed region) against scipy's result
+            ua = torch.as_tensor(u_start.reshape(n, n), device="cuda")
+            ub = model.step(ua)
+            rec["gpu_vs_scipy_same_step"] = {
+                "max_abs_diff": float(np.abs(ub.cpu().numpy().reshape(-1) - u_cpu).max()),
+                "state_max_abs": float(np.abs(u_cpu).max()),
+                "gpu_newton_its": model.last_stats["nit"], "scipy_newton_its": rec["newton_its"],
+                "bar": "1e-5 * max(1, |U|) (default f_tol)"}
+            del ua, ub, u_cpu
+            out["cpu_baseline"] = rec
         if world == 1 and args.extra == "on":
             out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet(),
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),

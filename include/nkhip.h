@@ -62,6 +62,9 @@ typedef struct nk_stats {
   double fnorm_2;      /* ||F(x)||_2 at exit */
   int32_t status;
   int32_t pad_;
+  int64_t n_backtrack; /* Newton iterations whose Armijo step s was < 1 (scalar_search_armijo,
+                          scipy/optimize/_linesearch.py:684-739) */
+  double step_min;     /* smallest accepted line-search step (1 when none backtracked) */
 } nk_stats;
 
 /* Per-kernel-class timings recorded with HIP events on the solver's stream. */
@@ -148,6 +151,12 @@ int nk_comm_create_rccl(nk_comm** out, const void* unique_id, int32_t rank, int3
  * logic on a single GPU): fills out[0..nranks-1]. */
 int nk_comm_create_loopback(nk_comm** out, int32_t nranks);
 int nk_comm_destroy(nk_comm* c);
+/* Marks the group failed: every rank blocked in, or later entering, a collective of this group
+ * returns NK_ECOMM instead of waiting for the failed rank (loopback: wakes the waiting threads;
+ * RCCL: the communicator is aborted with ncclCommAbort at destroy).  A stepper calls it itself
+ * when one of its steps fails with a negative code; a host thread that fails outside the
+ * library calls it before it exits. */
+int nk_comm_abort(nk_comm* c);
 
 /* ---------------- Swift-Hohenberg implicit time step (the north-star path) ---------------- */
 /* A stepper for one row slab [row0, row0+ny_local) of an ny_global x nx periodic grid.

@@ -531,16 +531,20 @@ struct Occ {
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_t(ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
   auto kern = arnoldi_kernel<NV, EXT, PF, NT>;
-  static Occ occ;  // per instantiation
-  if (occ.ncu == 0) {
+  // per instantiation, filled once by a thread-safe static initialiser (slab threads of the
+  // loopback communicator launch the same instantiation concurrently)
+  static const Occ occ = [&] {
+    Occ o;
     int dev = 0, ncu = 0, nb = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 64 * WPB, 0) != hipSuccess)
-      return hipErrorUnknown;
-    occ.blocks_per_cu = nb > 0 ? nb : 1;
-    occ.ncu = ncu > 0 ? ncu : 1;
-  }
+      return o;  // ncu == 0: reported below
+    o.blocks_per_cu = nb > 0 ? nb : 1;
+    o.ncu = ncu > 0 ? ncu : 1;
+    return o;
+  }();
+  if (occ.ncu == 0) return hipErrorUnknown;
   // one resident round of waves (NKHIP_ARN_ROUNDS scales it); bands of >= 8 rows, and no more
   // partial columns than the caller's buffer holds
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);

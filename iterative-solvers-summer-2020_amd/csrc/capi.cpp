@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <memory>
 #include <new>
 
@@ -179,6 +180,8 @@ int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, 
   A.out_w = w_out;
   const int nval = 2 * nv + 3;
   if (!dots) {  // no reduction wanted (timing): a persistent partial buffer, no synchronisation
+    static std::mutex mu;  // the buffer is shared by every caller thread
+    std::lock_guard<std::mutex> lk(mu);
     static double* buf = nullptr;
     static int64_t cap = 0;
     const int64_t need = int64_t(nval) * 65536;
@@ -292,6 +295,11 @@ int nk_comm_destroy(nk_comm* c) {
   delete c;
   return NK_OK;
 }
+int nk_comm_abort(nk_comm* c) {
+  if (!c) return NK_EINVAL;
+  c->abort();
+  return NK_OK;
+}
 
 // ------------------------------------------------------------------------------ SH stepper
 int nk_sh_create(nk_sh** out, int64_t ny_local, int64_t nx, int64_t ny_global, double h, double r,
@@ -338,8 +346,10 @@ int nk_sh_set_opts(nk_sh* s, const nk_opts* opts) {
 int nk_sh_step(nk_sh* s, const double* u_prev, double* u_next, nk_stats* stats) {
   if (!s || !u_prev || !u_next) return NK_EINVAL;
   int rc = s->P->prepare(u_prev);
-  if (rc) return rc;
-  return s->NK->solve(u_prev, u_next, stats);
+  if (!rc) rc = s->NK->solve(u_prev, u_next, stats);
+  // a failed rank must not leave its peers waiting in the next collective
+  if (rc < 0 && s->E->comm) s->E->comm->abort();
+  return rc;
 }
 
 int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {

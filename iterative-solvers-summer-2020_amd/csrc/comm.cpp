@@ -22,8 +22,16 @@ namespace {
 struct RcclComm final : nk_comm {
   ncclComm_t c = nullptr;
   int r = 0, p = 1;
+  double* bar = nullptr;  // barrier scratch, allocated on first use
+  bool aborted = false;
   ~RcclComm() override {
-    if (c) ncclCommDestroy(c);
+    if (c) {
+      if (aborted)
+        ncclCommAbort(c);
+      else
+        ncclCommDestroy(c);
+    }
+    if (bar) hipFree(bar);
   }
   int rank() const override { return r; }
   int size() const override { return p; }
@@ -44,23 +52,34 @@ struct RcclComm final : nk_comm {
     const size_t cnt = size_t(2 * nx);
     // Sends to one peer are matched in posting order, so with p == 2 (prev == next) the
     // neighbour's first receive (its lo) gets our last rows and its second (its hi) our first.
+    if (aborted) return NK_ECOMM;
     if (ncclGroupStart() != ncclSuccess) return NK_ECOMM;
-    ncclSend(v + (ny - 2) * nx, cnt, ncclDouble, next, c, s);
-    ncclSend(v, cnt, ncclDouble, prev, c, s);
-    ncclRecv(lo, cnt, ncclDouble, prev, c, s);
-    ncclRecv(hi, cnt, ncclDouble, next, c, s);
-    return ncclGroupEnd() == ncclSuccess ? NK_OK : NK_ECOMM;
+    // every call inside the group is checked; the group is closed in any case
+    ncclResult_t e = ncclSend(v + (ny - 2) * nx, cnt, ncclDouble, next, c, s);
+    if (e == ncclSuccess) e = ncclSend(v, cnt, ncclDouble, prev, c, s);
+    if (e == ncclSuccess) e = ncclRecv(lo, cnt, ncclDouble, prev, c, s);
+    if (e == ncclSuccess) e = ncclRecv(hi, cnt, ncclDouble, next, c, s);
+    const ncclResult_t g = ncclGroupEnd();
+    if (e != ncclSuccess || g != ncclSuccess) {
+      std::fprintf(stderr, "nkhip: RCCL halo failed: %s\n",
+                   ncclGetErrorString(e != ncclSuccess ? e : g));
+      return NK_ECOMM;
+    }
+    return NK_OK;
   }
 
   int barrier(hipStream_t s) override {
-    double* d = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double), s) != hipSuccess) return NK_EHIP;
-    hipMemsetAsync(d, 0, sizeof(double), s);
-    const ncclResult_t e = ncclAllReduce(d, d, 1, ncclDouble, ncclSum, c, s);
-    hipFreeAsync(d, s);
-    if (e != ncclSuccess) return NK_ECOMM;
+    if (aborted) return NK_ECOMM;
+    if (!bar && hipMalloc(reinterpret_cast<void**>(&bar), sizeof(double)) != hipSuccess) {
+      bar = nullptr;
+      return NK_EHIP;
+    }
+    if (hipMemsetAsync(bar, 0, sizeof(double), s) != hipSuccess) return NK_EHIP;
+    if (ncclAllReduce(bar, bar, 1, ncclDouble, ncclSum, c, s) != ncclSuccess) return NK_ECOMM;
     return hipStreamSynchronize(s) == hipSuccess ? NK_OK : NK_EHIP;
   }
+
+  void abort() override { aborted = true; }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -77,17 +96,26 @@ struct LoopShared {
   std::vector<const double*> vptr;
   std::vector<int64_t> vny;
   std::vector<std::vector<double>> vals;
+  bool aborted = false;
   explicit LoopShared(int np) : p(np), vptr(np), vny(np), vals(np) {}
-  void wait() {
+  // false once any rank has aborted the group (then nobody waits for the missing rank)
+  bool wait() {
     std::unique_lock<std::mutex> lk(m);
+    if (aborted) return false;
     const int64_t g = gen;
     if (++arrived == p) {
       arrived = 0;
       ++gen;
       cv.notify_all();
-    } else {
-      cv.wait(lk, [&] { return gen != g; });
+      return true;
     }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return gen != g;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m);
+    aborted = true;
+    cv.notify_all();
   }
 };
 
@@ -101,10 +129,12 @@ struct LoopComm final : nk_comm {
     std::vector<double> host(nv);
     if (hipMemcpyAsync(host.data(), dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) !=
             hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+        hipStreamSynchronize(s) != hipSuccess) {
+      sh->abort();
       return NK_EHIP;
+    }
     sh->vals[r] = host;
-    sh->wait();
+    if (!sh->wait()) return NK_ECOMM;
     for (int k = 0; k < nv; ++k) {
       double acc = sh->vals[0][k];
       for (int q = 1; q < sh->p; ++q) {
@@ -116,7 +146,7 @@ struct LoopComm final : nk_comm {
       }
       host[k] = acc;
     }
-    sh->wait();
+    if (!sh->wait()) return NK_ECOMM;
     if (hipMemcpyAsync(dev, host.data(), sizeof(double) * nv, hipMemcpyHostToDevice, s) !=
             hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
@@ -127,24 +157,36 @@ struct LoopComm final : nk_comm {
   int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
            hipStream_t s) override {
     const int p = sh->p, prev = (r - 1 + p) % p, next = (r + 1) % p;
-    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) {
+      sh->abort();
+      return NK_EHIP;
+    }
     sh->vptr[r] = v;
     sh->vny[r] = ny;
-    sh->wait();
+    if (!sh->wait()) return NK_ECOMM;
     const size_t bytes = sizeof(double) * size_t(2 * nx);
     hipError_t e = hipMemcpyAsync(lo, sh->vptr[prev] + (sh->vny[prev] - 2) * nx, bytes,
                                   hipMemcpyDeviceToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(hi, sh->vptr[next], bytes, hipMemcpyDeviceToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    sh->wait();  // nobody may overwrite its slab before every neighbour has copied
-    return e == hipSuccess ? NK_OK : NK_EHIP;
+    // nobody may overwrite its slab before every neighbour has copied
+    if (!sh->wait()) return NK_ECOMM;
+    if (e != hipSuccess) {
+      sh->abort();
+      return NK_EHIP;
+    }
+    return NK_OK;
   }
 
   int barrier(hipStream_t s) override {
-    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
-    sh->wait();
-    return NK_OK;
+    if (hipStreamSynchronize(s) != hipSuccess) {
+      sh->abort();
+      return NK_EHIP;
+    }
+    return sh->wait() ? NK_OK : NK_ECOMM;
   }
+
+  void abort() override { sh->abort(); }
 };
 
 }  // namespace

@@ -23,6 +23,10 @@ struct nk_comm {
   virtual int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
                    hipStream_t s) = 0;
   virtual int barrier(hipStream_t s) = 0;
+  // A rank that fails outside the collective calls (a HIP error, an exception in its host
+  // thread) marks the group aborted: peers blocked in (or entering) a collective return
+  // NK_ECOMM instead of waiting forever.  RCCL: ncclCommAbort.
+  virtual void abort() = 0;
 };
 
 namespace nk {

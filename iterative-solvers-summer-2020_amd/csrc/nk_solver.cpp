@@ -356,6 +356,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
   nk_stats dummy;
   st_ = st ? st : &dummy;
   std::memset(st_, 0, sizeof(nk_stats));
+  st_->step_min = 1.0;
   ocount_ = 0;
   ohead_ = 0;
   const int64_t n = E_.n;
@@ -407,6 +408,8 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
     double s = 1.0, fnorm_new = 0.0;
     rc = line_search(&s, &fnorm_new, &fmax, &xmax);
     if (rc) break;
+    if (s != 1.0) st_->n_backtrack += 1;
+    st_->step_min = std::min(st_->step_min, s);
     std::swap(X_, Xt_);
     std::swap(Fx_, Ft_);
     std::swap(G0_, Gt_);

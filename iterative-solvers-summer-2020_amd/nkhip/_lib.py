@@ -35,7 +35,8 @@ class nk_opts(C.Structure):
 class nk_stats(C.Structure):
     _fields_ = [("nit", C.c_int64), ("nfev", C.c_int64), ("njvp", C.c_int64),
                 ("n_arnoldi", C.c_int64), ("fnorm_inf", C.c_double), ("fnorm_2", C.c_double),
-                ("status", C.c_int32), ("pad_", C.c_int32)]
+                ("status", C.c_int32), ("pad_", C.c_int32), ("n_backtrack", C.c_int64),
+                ("step_min", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad_"}
@@ -94,6 +95,7 @@ SIGNATURES = [
     ("nk_comm_create_rccl", C.c_int, [C.POINTER(_P), _P, _I32, _I32]),
     ("nk_comm_create_loopback", C.c_int, [C.POINTER(_P), _I32]),
     ("nk_comm_destroy", C.c_int, [_P]),
+    ("nk_comm_abort", C.c_int, [_P]),
     ("nk_sh_create", C.c_int, [C.POINTER(_P), _I64, _I64, _I64, _D, _D, _D, _D,
                                C.POINTER(nk_opts), _P, _P]),
     ("nk_sh_destroy", C.c_int, [_P]),

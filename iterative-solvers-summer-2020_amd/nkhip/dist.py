@@ -42,6 +42,12 @@ class Comm:
         self.rank = rank
         self.size = size
 
+    def abort(self):
+        """Mark the group failed: peers blocked in a collective return NK_ECOMM (nk_comm_abort).
+        A host thread driving a slab calls this when it fails, before it exits."""
+        if self.handle:
+            lib.nk_comm_abort(self.handle)
+
     def close(self):
         if self.handle:
             lib.nk_comm_destroy(self.handle)

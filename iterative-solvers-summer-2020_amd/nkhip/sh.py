@@ -85,14 +85,31 @@ class SwiftHohenberg:
         return U.contiguous()
 
     def step(self, U, out=None):
-        """One implicit Crank-Nicolson step U[s] -> U[s+1] (sh_scipy_nk.py:56-61)."""
+        """One implicit Crank-Nicolson step U[s] -> U[s+1] (sh_scipy_nk.py:56-61).
+
+        ``out`` (optional) must be a contiguous float64 CUDA tensor with as many values as the
+        slab; it may alias ``U``.  The library runs on the stepper's stream: when that is not
+        torch's current stream, it first waits for the work torch has queued (U, out), and torch's
+        stream waits for the step before anything reads ``out``."""
         U = self._as_grid(U)
         if U.numel() != self.ny_local * self.nx:
             raise ValueError(f"state has {U.numel()} values, slab is {self.ny_local}x{self.nx}")
-        out = torch.empty_like(U) if out is None else out
+        if out is None:
+            out = torch.empty_like(U)
+        elif (not isinstance(out, torch.Tensor) or out.device.type != "cuda"
+              or out.device != U.device or out.dtype != torch.float64
+              or out.numel() != U.numel() or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous float64 CUDA tensor on the state's device "
+                             f"with {U.numel()} values")
+        cur = torch.cuda.current_stream(U.device)
+        mine = self._stream if self._stream is not None else cur
+        if mine != cur:
+            mine.wait_stream(cur)
         st = _lib.nk_stats()
         rc = lib.nk_sh_step(self._h, C.c_void_p(U.data_ptr()), C.c_void_p(out.data_ptr()),
                             C.byref(st))
+        if mine != cur:
+            cur.wait_stream(mine)
         self.last_stats = st.as_dict()
         if rc == _lib.NK_NO_CONVERGENCE:
             raise NoConvergence(out)

@@ -56,6 +56,7 @@ class _Stats:
         self.njvp = 0
         self.nit = 0
         self.arnoldi = 0
+        self.steps = []  # accepted line-search step s per Newton iteration
 
 
 def _givens(a, b):
@@ -311,6 +312,7 @@ def newton_krylov(F, xin, *, rdiff=None, inner_m=30, outer_k=10, verbose=False, 
             x = x + dx
             Fx = func(x)
             Fx_norm_new = _norm(Fx)
+        stats.steps.append(s)
         jac.update(x.copy(), Fx)
         eta_A = gamma * Fx_norm_new ** 2 / Fx_norm ** 2
         if gamma * eta ** 2 < eta_treshold:

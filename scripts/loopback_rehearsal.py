@@ -54,6 +54,7 @@ def main():
                     m.close()
             except BaseException as e:  # noqa: BLE001
                 errs.append(repr(e))
+                comms[p].abort()  # peers leave their collectives instead of blocking
 
         t0 = time.perf_counter()
         th = [threading.Thread(target=run, args=(p,)) for p in range(P)]
@@ -62,6 +63,9 @@ def main():
         for t in th:
             t.join(timeout=600)
         dt = time.perf_counter() - t0
+        if any(t.is_alive() for t in th):
+            print(json.dumps({"slabs": P, "errors": ["slab thread still running"]}), flush=True)
+            os._exit(1)  # a blocked thread may still touch the comms: do not close them
         for c in comms:
             c.close()
         if errs:

@@ -25,3 +25,36 @@ def load_golden(name):
 @pytest.fixture
 def golden():
     return load_golden
+
+
+def run_slabs(comms, body, timeout=300):
+    """Drive one slab per host thread (loopback communicator): body(p) for p in ranks.
+
+    A rank that raises aborts the group (nk_comm_abort), so its peers leave their collectives
+    with NK_ECOMM instead of blocking; the first error is re-raised after every thread has
+    ended.  A thread still alive after `timeout` fails the test (the comms are then NOT closed:
+    a blocked thread may still touch them)."""
+    import threading
+    errs = []
+
+    def run(p):
+        try:
+            body(p)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            comms[p].abort()
+
+    th = [threading.Thread(target=run, args=(p,), daemon=True) for p in range(len(comms))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=timeout)
+    alive = [p for p, t in enumerate(th) if t.is_alive()]
+    if alive:
+        for c in comms:
+            c.abort()
+        raise AssertionError(f"slab threads {alive} still running after {timeout} s")
+    for c in comms:
+        c.close()
+    if errs:
+        raise errs[0]

@@ -43,8 +43,11 @@ def set_old(ns, uo):
     ns["UoUoUo"] = np.multiply(uo, ns["UoUo"])
 
 
-def nk_step(ns, uo, **kw):
-    """One step of the reference loop (sh_scipy_nk.py:56-61), counting F evals and Newton its."""
+def nk_step(ns, uo, steps=None, **kw):
+    """One step of the reference loop (sh_scipy_nk.py:56-61), counting F evals and Newton its.
+    `steps` (a list) receives the Armijo step size s of every Newton iteration: scipy's own
+    scalar_search_armijo (scipy/optimize/_linesearch.py:684-739) is wrapped, not replaced."""
+    import scipy.optimize._nonlin as nonlin
     from scipy.optimize import newton_krylov
     set_old(ns, uo)
     nfev = [0]
@@ -58,7 +61,19 @@ def nk_step(ns, uo, **kw):
     def cb(x, f):
         nit[0] += 1
 
-    u = newton_krylov(F, uo, callback=cb, **kw)
+    orig = nonlin.scalar_search_armijo
+
+    def armijo(*a, **k):
+        out = orig(*a, **k)
+        if steps is not None:
+            steps.append(np.nan if out[0] is None else float(out[0]))
+        return out
+
+    nonlin.scalar_search_armijo = armijo
+    try:
+        u = newton_krylov(F, uo, callback=cb, **kw)
+    finally:
+        nonlin.scalar_search_armijo = orig
     set_old(ns, uo)
     fin = float(np.abs(res(u)).max())
     return u, nit[0], nfev[0], fin
@@ -72,8 +87,29 @@ def ops_case(N, d, seed=2020):
                 lap_v=ns["Lap"] @ v, L_v=ns["L"] @ v, L_nnz=ns["L"].nnz)
 
 
+def backtrack_case():
+    """(4) A Newton step whose Armijo line search backtracks (s < 1, including the cubic branch
+    of scalar_search_armijo): the reference geometry (N = 61, d = 40) from a large-amplitude
+    start U0 = 3 * default_rng(2020).standard_normal(N^2), default f_tol.  Records scipy's step
+    sizes per Newton iteration and its F-eval count."""
+    N, d = 61, 40.0
+    ns = reference_namespace(N, d)
+    U0 = 3.0 * np.random.default_rng(2020).standard_normal(N * N)
+    steps = []
+    U, nit, nfev, fin = nk_step(ns, U0, steps=steps)
+    print("nk_n61_amp3_backtrack nit", nit, "nfev", nfev, "steps", np.round(steps, 4))
+    return dict(N=N, d=d, h=ns["h"], r=0.01, k=0.2, g=1.0, f_tol=np.nan,
+                traj=np.array([U0, U]), nit=np.array([nit]), nfev=np.array([nfev]),
+                fnorm=np.array([fin]), steps=np.array(steps))
+
+
 def main():
-    cases = {}
+    if "--only-backtrack" in sys.argv:
+        z = backtrack_case()
+        np.savez_compressed(os.path.join(OUT, "nk_n61_amp3_backtrack.npz"),
+                            **{k: np.asarray(v) for k, v in z.items()})
+        return 0
+    cases = {"nk_n61_amp3_backtrack": backtrack_case()}
     # (1) operator fixtures: L@v and Lap@v at N = 5 (C++ twin geometry d=2, main.cpp:3-5),
     #     61 and 64 (reference domain d=40), plus an h = 0.625 grid at N = 128.
     for name, (N, d) in {"ops_n5_d2": (5, 2.0), "ops_n61": (61, 40.0), "ops_n64": (64, 40.0),

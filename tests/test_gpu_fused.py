@@ -125,40 +125,30 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx):
     """Row slabs through the fused kernel: every rank evaluates y on its edge rows, the loopback
     communicator exchanges them (the RCCL path's protocol), and the fused pass takes them as its
     halo rows.  Same root as the single periodic slab, and the fused kernel did run on each slab."""
-    import threading
     import nkhip
+    from conftest import run_slabs
     U0 = np.random.default_rng(7).standard_normal((ny_total, nx))
     single = nkhip.SwiftHohenberg(N=nx, ny=ny_total, d=0.625 * nx, f_tol=1e-10)
     ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
     ref_nit = single.last_stats["nit"]
     single.close()
     comms = nkhip.loopback_comms(nranks)
-    out, profs, nits, errs = [None] * nranks, [None] * nranks, [None] * nranks, []
+    out, profs, nits = [None] * nranks, [None] * nranks, [None] * nranks
 
     def run(p):
-        try:
-            stream = torch.cuda.Stream()
-            with torch.cuda.stream(stream):
-                row0, ny = nkhip.slab_rows(ny_total, p, nranks)
-                m = nkhip.SwiftHohenberg(N=nx, ny=ny_total, d=0.625 * nx, f_tol=1e-10,
-                                         comm=comms[p], ny_local=ny, stream=stream)
-                u = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
-                out[p] = m.step(u).cpu().numpy()
-                nits[p] = m.last_stats["nit"]
-                profs[p] = m.kernel_profile()
-                stream.synchronize()
-                m.close()
-        except BaseException as e:  # noqa: BLE001
-            errs.append(e)
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            row0, ny = nkhip.slab_rows(ny_total, p, nranks)
+            m = nkhip.SwiftHohenberg(N=nx, ny=ny_total, d=0.625 * nx, f_tol=1e-10,
+                                     comm=comms[p], ny_local=ny, stream=stream)
+            u = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
+            out[p] = m.step(u).cpu().numpy()
+            nits[p] = m.last_stats["nit"]
+            profs[p] = m.kernel_profile()
+            stream.synchronize()
+            m.close()
 
-    th = [threading.Thread(target=run, args=(p,)) for p in range(nranks)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=300)
-    for c in comms:
-        c.close()
-    assert not errs, errs
+    run_slabs(comms, run)
     for pr in profs:
         assert pr["arnoldi_fused"]["launches"] > 0
         assert pr["arnoldi_edge"]["launches"] == pr["arnoldi_fused"]["launches"]

@@ -6,19 +6,18 @@ summation order, Gram-based MGS), so parity is judged on the converged root:
   * default f_tol (eps^(1/3)):  <= 1e-5 * max(1, |U_ref|_inf)
   * Newton iteration counts within +-1 of scipy's in FD (scipy-faithful) mode.
 """
-import threading
-
 import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
+from conftest import load_golden, run_slabs
 from oracle import sh_oracle
 
 pytestmark = pytest.mark.gpu
 
 CASES = ["nk_n61_default", "nk_n61_tight", "nk_n64_default", "nk_n64_h0625_tight",
-         "nk_n96_h0625_tight", "nk_n5_d2_tight"]
+         "nk_n96_h0625_tight", "nk_n5_d2_tight", "nk_n61_amp3_backtrack"]
+TIGHT = [c for c in CASES if c.endswith("tight")]
 
 
 def _model(z, **kw):
@@ -56,6 +55,47 @@ def test_sh_step_matches_scipy(name, jvp):
         bound = ftol if ftol is not None else 6.06e-6
         assert np.abs(F).max() <= 10 * bound
     m.close()
+
+
+@pytest.mark.parametrize("name", TIGHT)
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_sh_step_fevals_match_scipy(name, fused, monkeypatch):
+    """scipy's nfev counts every call of F: the initial one, one per KrylovJacobian.matvec and
+    the line-search evaluations.  The GPU solver counts the same calls as nfev + njvp (the JVPs
+    of the fused Arnoldi step are the closed form of that difference quotient)."""
+    monkeypatch.setenv("NKHIP_FUSED", fused)
+    z = load_golden(name)
+    m, ftol = _model(z, jvp="fd")
+    N = int(z["N"])
+    U = torch.as_tensor(z["traj"][0].reshape(N, N), device="cuda")
+    for s in range(len(z["traj"]) - 1):
+        U = m.step(U)
+        st = m.last_stats
+        assert st["status"] == 0
+        got, ref = st["nfev"] + st["njvp"], int(z["nfev"][s])
+        assert abs(got - ref) <= 1, (s, got, ref, st)
+    m.close()
+
+
+def test_line_search_backtracks_like_scipy():
+    """SURVEY 8a row A9 on the GPU: the reference's Newton step from a large-amplitude start
+    backtracks in 5 of its 13 iterations (quadratic and cubic branches of scalar_search_armijo).
+    The inexact Newton directions (eta ~ 0.9) carry FD rounding noise, so steps agree to a few
+    per cent, not bitwise (the CPU restatement: ~1 %); the backtracking count is exact."""
+    z = load_golden("nk_n61_amp3_backtrack")
+    m, _ = _model(z, jvp="fd")
+    N = int(z["N"])
+    U = m.step(torch.as_tensor(z["traj"][0].reshape(N, N), device="cuda"))
+    st = m.last_stats
+    m.close()
+    steps = z["steps"]
+    assert st["status"] == 0
+    assert st["n_backtrack"] == int((steps < 1).sum()), (st, steps)
+    assert abs(st["step_min"] - steps.min()) <= 0.05 * steps.min(), (st, steps)
+    assert abs(st["nit"] - int(z["nit"][0])) <= 1
+    ref_f = int(z["nfev"][0])
+    assert abs(st["nfev"] + st["njvp"] - ref_f) <= 0.05 * ref_f, (st, ref_f)
+    _check(U.cpu().numpy().reshape(-1), z["traj"][1], None)
 
 
 def test_generic_newton_krylov_dropin():
@@ -126,32 +166,21 @@ def test_loopback_slabs_match_single_slab(nranks, N):
     ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
     comms = nkhip.loopback_comms(nranks)
     out = [None] * nranks
-    errs = []
 
     def run(p):
-        try:
-            stream = torch.cuda.Stream()
-            with torch.cuda.stream(stream):
-                row0, ny = nkhip.slab_rows(N, p, nranks)
-                m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comms[p],
-                                         ny_local=ny, stream=stream)
-                u = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
-                out[p] = m.step(u).cpu().numpy()
-                stream.synchronize()
-                m.close()
-        except BaseException as e:  # noqa: BLE001
-            errs.append(e)
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            row0, ny = nkhip.slab_rows(N, p, nranks)
+            m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comms[p],
+                                     ny_local=ny, stream=stream)
+            u = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
+            out[p] = m.step(u).cpu().numpy()
+            stream.synchronize()
+            m.close()
 
-    th = [threading.Thread(target=run, args=(p,)) for p in range(nranks)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=300)
-    assert not errs, errs
+    run_slabs(comms, run)
     got = np.concatenate(out, axis=0)
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
-    for c in comms:
-        c.close()
 
 
 def test_large_grid_root_property():
@@ -166,6 +195,38 @@ def test_large_grid_root_property():
     F = sh_oracle.residual(U1.cpu().numpy().reshape(-1), U0.reshape(-1), N, N, 0.625, 0.01, 0.2,
                            1.0)
     assert np.abs(F).max() <= 6.06e-6 * 1.01
+
+
+def test_config4_4096_step():
+    """BASELINE config 4 (the bench workload): one 4096^2 FD step from default_rng(2020), scipy
+    default f_tol.  The result is a root of the oracle residual (sh_scipy_nk.py:47-49) to the
+    max-norm tolerance, and the unfused two-evaluation path (NKHIP_FUSED=0) reaches the same
+    root: |dU| <= 1e-5 max(1, |U|)."""
+    import os
+    import nkhip
+    N = 4096
+    U0 = np.random.default_rng(2020).standard_normal((N, N))
+    out = {}
+    for fused in ("1", "0"):
+        os.environ["NKHIP_FUSED"] = fused
+        try:
+            m = nkhip.SwiftHohenberg(N=N, d=0.625 * N)
+            U1 = m.step(torch.as_tensor(U0, device="cuda"))
+            st = dict(m.last_stats)
+            prof = m.kernel_profile()
+            m.close()
+        finally:
+            os.environ.pop("NKHIP_FUSED", None)
+        assert st["status"] == 0 and 2 <= st["nit"] <= 10, st
+        assert (prof["arnoldi_fused"]["launches"] > 0) == (fused == "1")
+        out[fused] = U1.cpu().numpy()
+        del U1
+        torch.cuda.empty_cache()
+        F = sh_oracle.residual(out[fused].reshape(-1), U0.reshape(-1), N, N, 0.625, 0.01, 0.2,
+                               1.0)
+        assert np.abs(F).max() <= 1.01 * np.finfo(float).eps ** (1 / 3), (fused, np.abs(F).max())
+    scale = max(1.0, float(np.abs(out["0"]).max()))
+    assert float(np.abs(out["1"] - out["0"]).max()) <= 1e-5 * scale
 
 
 def test_rccl_world1_matches_single_slab():

@@ -161,3 +161,21 @@ def test_march_and_point_kernels_agree_bitwise():
     out = torch.zeros(64 * 66 + 1, dtype=torch.float64, device="cuda")
     nkhip.sh13_apply(buf[1:], h, r, 64, 66, out=out[1:])
     assert np.array_equal(y_march.reshape(-1), out[1:].cpu().numpy())
+
+
+@pytest.mark.parametrize("op", ["lap5", "sh13"])
+def test_config2_1024(op):
+    """BASELINE config 2: the 1024^2 fp64 periodic Laplacian (and the 13-point L) on the grid
+    and input the bench measures (v = default_rng(7).standard_normal, h = 0.625) vs the oracle
+    stencils, themselves pinned to the reference's CSR matrices (test_oracle.py)."""
+    import nkhip
+    n, h, r = 1024, 0.625, 0.01
+    v_np = np.random.default_rng(7).standard_normal(n * n)
+    v = torch.as_tensor(v_np.reshape(n, n), device="cuda")
+    if op == "lap5":
+        y = nkhip.lap5_apply(v, 1 / h ** 2).cpu().numpy().reshape(-1)
+        ref = sh_oracle.lap5(v_np, n, n, 1 / h ** 2)
+    else:
+        y = nkhip.sh13_apply(v, h, r).cpu().numpy().reshape(-1)
+        ref = sh_oracle.sh13(v_np, n, n, h, r)
+    assert np.abs(y - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
