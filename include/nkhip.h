@@ -128,6 +128,21 @@ int nk_sh_arnoldi_fused(const double* const* V_dev, const double* coef, int32_t 
                         double g, double zs, double sc, double* v_out_dev, double* w_out_dev,
                         double* dots, void* stream);
 
+/* Edge arrays (the fused step's block halos, 1/64 of a grid vector): for every column group
+ * boundary B = 256 b and row q, E[(b*ny + q)*4 + 0..3] = v[q][B-2], v[q][B-1], v[q][B], v[q][B+1]
+ * (columns mod nx); nk_edge_elems() doubles, nx even. */
+int64_t nk_edge_elems(int64_t ny, int64_t nx);
+int nk_edge_gather(const double* v_dev, double* E_dev, int64_t ny, int64_t nx, void* stream);
+/* nk_sh_arnoldi_fused with the block halos read from the entries' edge arrays E_dev[0..nv]
+ * (those of V[0..nv-1], then of w) instead of from the vectors (same values, identical results),
+ * and the edge arrays of v_out / w_out written (Ev_out / Ew_out, each may be NULL). */
+int nk_sh_arnoldi_fused_edges(const double* const* V_dev, const double* const* E_dev,
+                              const double* coef, int32_t nv, const double* w_dev, double tau,
+                              const double* x0_dev, const double* G0_dev, const double* z_dev,
+                              int64_t ny, int64_t nx, double h, double r, double k, double g,
+                              double zs, double sc, double* v_out_dev, double* w_out_dev,
+                              double* Ev_out_dev, double* Ew_out_dev, double* dots, void* stream);
+
 /* ---------------- BLAS-1 (scipy get_blas_funcs dot/nrm2/axpy/scal in _gcrotmk.py:104-126) ------ */
 /* Scalar results are written to host memory; the call synchronises `stream`. */
 int nk_dot(const double* x_dev, const double* y_dev, int64_t n, double* out, void* stream);

@@ -48,8 +48,12 @@ namespace {
 #define ARN_DPPNB 1
 #endif
 
-constexpr int kSW = 64;  // columns per wave (one per lane)
-constexpr int WPB = 4;   // waves per block
+#ifndef ARN_WPB
+#define ARN_WPB 4
+#endif
+constexpr int kSW = 64;       // columns per wave (one per lane)
+constexpr int WPB = ARN_WPB;  // waves per block (the packed halo loads carry 16 * WPB entries)
+static_assert(WPB * kSW == kEdgeW, "edge arrays are laid out for the fused kernel's blocks");
 
 __device__ __forceinline__ double applyL13(const SHCoef& k, double c, double a1, double dg,
                                            double a2) {
@@ -235,6 +239,30 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     hp = p;
     hcf = cf;
   }
+  // the same entry's edge array (its left pair at boundary grp, its right pair at grp + 1)
+  const bool useE = A.E[0] != nullptr;
+  const double* hE;
+  {
+    const int e = wid + WPB * (lane >> 2);
+    const double* p = A.E[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) p = (e == j) ? A.E[j] : p;
+    hE = p;
+  }
+  const int64_t grpR = (grp + 1 < ngroups) ? grp + 1 : 0;
+  // edge-array stores of the outputs: the lane holding columns B, B+1 of a boundary B writes
+  // them as E[b][q][2..3]; the lane holding B-2, B-1 as E[b][q][0..1] (b = 0 for nx - 2, nx - 1)
+  const int64_t nbE = ngroups;
+  const bool eL = own && (c % kEdgeW == 0);
+  const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
+  const int64_t ebo = eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
+  const bool eOn = eL || eR;
+  const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
+  // byte offset of this lane's edge pair at row q (kOOB: nothing to store)
+  auto eoff = [&](int64_t q) -> uint32_t {
+    return eOn ? uint32_t(((ebo / 4) * ny * 4 + q * 4 + (ebo & 3)) * 8) : kOOB;
+  };
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
   // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their u arrives in A.yh (the x0 entry
   // and the x0 halo lanes read it there in place of x0)
@@ -248,7 +276,8 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 
   struct Slot {
     dv2 e[NI];
-    double hv, hx;
+    double hv;
+    double hx;
     bool own;  // row of this slab (false: a neighbour's halo row, u taken from A.yh)
   };
   auto load = [&](Slot& s, int64_t q) {
@@ -268,7 +297,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
         s.e[k] = *p;
     }
     const int64_t ho = qq * nx + hcol;
-    if constexpr (!EXT) s.hv = hp[ho];
+    // block halo: from the entry's edge array (four rows per line) or from the vector itself
+    const int64_t eo = ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh;
+    if constexpr (!EXT) s.hv = *(useE ? hE + eo : hp + ho);
     s.hx = *((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
     s.own = !hrow;
   };
@@ -396,6 +427,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
                                            st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
+    if (A.Eout_v)  // wave-uniform
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
+                                             st ? eoff(q) : kOOB, 0, 0);
     return dv2{cm2 + cp2, cm1 + cp3};  // h2 of row q
   };
 
@@ -432,6 +466,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
                                            (in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB,
                                            0, 0);
+    if (A.Eout_w)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
+                                             (in && hf == 0) ? eoff(r) : kOOB, 0, 0);
     const dv2 wm = in ? wo : dv2{0.0, 0.0};
     const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
 #pragma unroll
@@ -531,6 +568,7 @@ struct Occ {
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_t(ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
   auto kern = arnoldi_kernel<NV, EXT, PF, NT>;
+  if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
   // per instantiation, filled once by a thread-safe static initialiser (slab threads of the
   // loopback communicator launch the same instantiation concurrently)
   static const Occ occ = [&] {
@@ -650,7 +688,31 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
   y4[int64_t(t) * A.nx + j] = y;
 }
 
+// E[(b ny + q) 4 + 0..3] = v[q][B-2], v[q][B-1], v[q][B], v[q][B+1], B = kEdgeW b, columns mod nx
+__global__ void __launch_bounds__(256) edge_gather_kernel(const double* __restrict__ v,
+                                                          double* __restrict__ E, int64_t ny,
+                                                          int64_t nx, int64_t nb) {
+  const int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x;  // t = b ny + q
+  if (t >= nb * ny) return;
+  const int64_t b = t / ny, q = t - b * ny;
+  const int64_t B = b * kEdgeW;
+  const double* row = v + q * nx;
+  const int64_t cl = (B >= 2) ? B - 2 : B - 2 + nx;
+  dv2 lo{row[cl], row[cl + 1]};  // B - 2 and B - 1 (even nx: a pair never straddles the wrap)
+  dv2 hi{row[B], row[B + 1]};
+  reinterpret_cast<dv2*>(E)[2 * t] = lo;
+  reinterpret_cast<dv2*>(E)[2 * t + 1] = hi;
+}
+
 }  // namespace
+
+hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx, hipStream_t s) {
+  if (!v || !E || ny < 1 || nx < 4 || nx % 2) return hipErrorInvalidValue;
+  const int64_t nb = edge_groups(nx);
+  hipLaunchKernelGGL(edge_gather_kernel, dim3(unsigned((nb * ny + 255) / 256)), dim3(256), 0, s,
+                     v, E, ny, nx, nb);
+  return hipGetLastError();
+}
 
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) {
   if (A.ny < 4 || A.nx < 1 || !y4) return hipErrorInvalidValue;

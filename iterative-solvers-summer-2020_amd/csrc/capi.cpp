@@ -152,14 +152,24 @@ int nk_sh_fdjvp(const double* x0, const double* G0, const double* z, double* y, 
   return hip_rc(stencil_launch(SMode::FDJVP, A, S(stream), nullptr));
 }
 
-int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, const double* w,
-                        double tau, const double* x0, const double* G0, const double* z,
-                        int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
-                        double sc, double* v_out, double* w_out, double* dots, void* stream) {
+namespace {
+int arnoldi_fused_call(const double* const* V, const double* const* E, const double* coef,
+                       int32_t nv, const double* w, double tau, const double* x0, const double* G0,
+                       const double* z, int64_t ny, int64_t nx, double h, double r, double k,
+                       double g, double zs, double sc, double* v_out, double* w_out,
+                       double* Ev_out, double* Ew_out, double* dots, void* stream) {
   // G0 is not read (closed-form difference quotient) and may be NULL
   if (!V || !coef || !w || !x0 || !v_out || !w_out || !(sc != 0.0)) return NK_EINVAL;
   if (!arnoldi_supported(nv, ny, nx)) return NK_EINVAL;
   ArnoldiArgs A;
+  if (E) {
+    for (int i = 0; i <= nv; ++i) {
+      if (!E[i]) return NK_EINVAL;
+      A.E[i] = E[i];
+    }
+  }
+  A.Eout_v = Ev_out;
+  A.Eout_w = Ew_out;
   A.ny = ny;
   A.nx = nx;
   A.nv = nv;
@@ -204,6 +214,35 @@ int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, 
                        A.partial_cap = int64_t(nval) * (65536 + 1);
                        return arnoldi_launch(A, S(stream), nb);
                      });
+}
+}  // namespace
+
+int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, const double* w,
+                        double tau, const double* x0, const double* G0, const double* z,
+                        int64_t ny, int64_t nx, double h, double r, double k, double g, double zs,
+                        double sc, double* v_out, double* w_out, double* dots, void* stream) {
+  return arnoldi_fused_call(V, nullptr, coef, nv, w, tau, x0, G0, z, ny, nx, h, r, k, g, zs, sc,
+                            v_out, w_out, nullptr, nullptr, dots, stream);
+}
+
+int nk_sh_arnoldi_fused_edges(const double* const* V, const double* const* E, const double* coef,
+                              int32_t nv, const double* w, double tau, const double* x0,
+                              const double* G0, const double* z, int64_t ny, int64_t nx, double h,
+                              double r, double k, double g, double zs, double sc, double* v_out,
+                              double* w_out, double* Ev_out, double* Ew_out, double* dots,
+                              void* stream) {
+  if (!E) return NK_EINVAL;
+  return arnoldi_fused_call(V, E, coef, nv, w, tau, x0, G0, z, ny, nx, h, r, k, g, zs, sc, v_out,
+                            w_out, Ev_out, Ew_out, dots, stream);
+}
+
+int64_t nk_edge_elems(int64_t ny, int64_t nx) {
+  return (ny > 0 && nx > 0) ? edge_elems(ny, nx) : NK_EINVAL;
+}
+
+int nk_edge_gather(const double* v, double* E, int64_t ny, int64_t nx, void* stream) {
+  if (!v || !E || ny < 1 || nx < 4 || nx % 2) return NK_EINVAL;
+  return hip_rc(edge_gather_launch(v, E, ny, nx, S(stream)));
 }
 
 // ------------------------------------------------------------------------------ BLAS-1
@@ -353,14 +392,10 @@ int nk_sh_step(nk_sh* s, const double* u_prev, double* u_next, nk_stats* stats) 
 }
 
 int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max) {
-  static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
-                                         "krylov_mdot", "krylov_combo", "reduce_final", "copy",
-                                         "halo", "user_F", "axpby", "arnoldi_fused",
-                                         "arnoldi_edge"};
   if (!s) return NK_EINVAL;
   for (int k = 0; k < K_NKINDS && k < max; ++k) {
     std::memset(out[k].name, 0, sizeof(out[k].name));
-    std::strncpy(out[k].name, names[k], sizeof(out[k].name) - 1);
+    std::strncpy(out[k].name, kind_name(k), sizeof(out[k].name) - 1);
     out[k].launches = s->E->stat(k).launches;
     out[k].total_ms = s->E->stat(k).ms;
     out[k].alg_bytes = s->E->stat(k).bytes;

@@ -56,6 +56,7 @@ int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bo
     rc = P_.jvp(X_, G0_, z, zs, omega_ / znorm, w);
     st_->njvp += 1;
   }
+  if (!rc) rc = P_.publish_edges(w);  // w enters the update of the next (fused) step
   if (rc) return rc;
   st_->n_arnoldi += 1;
   // one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i <= j, the diagonal is |v_j|^2), |w|^2
@@ -233,6 +234,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
       rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
         return combo_launch(w, w, tau, U, j + 1, n, nullptr, E_.s, &nblk);
       });
+      if (!rc) rc = P_.publish_edges(w);  // v_{j+1}, a basis vector of later fused steps
       if (rc) return rc;
       const double* z;
       double zs, zn;
@@ -259,6 +261,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     });
     // only |v_{j+1}|^2 is used (a non-finite v shows up in it): one sum, one all-reduce on N GPUs
     if (!rc) rc = E_.reduce_async(nblk, 1, 1, Engine::kSlotCombo);
+    if (!rc) rc = P_.publish_edges(w);
     if (rc) return rc;
     // speculatively start step j+1 with its scale taken from the device norm
     const bool spec = next_is_v && P_.has_dev_scale() && P_.may_speculate();

@@ -118,6 +118,18 @@ hipError_t axpby_launch(double a, const double* x, double b, const double* y, do
 // Fused Arnoldi step (arnoldi.hip): update v = tau*w + sum c_i V_i, FD JVP w' of z = v (or of an
 // external z), and the multi-dot of w' and v against V and v, in one launch (periodic grid only).
 constexpr int kArnMaxNV = 35;
+// Edge arrays: the fused kernel's blocks own kEdgeW-column groups and read the two columns
+// either side of each group of every update entry (its block halo).  Read straight from the
+// vectors those are two extra lines per entry and row that the NEIGHBOUR block streams (a
+// non-temporal load away from L2): ~9 % of the launch (profiles/r02_arnoldi_ab.md).  An edge
+// array holds, per group boundary b (column B = kEdgeW b) and row q, the four values
+// v[q][B-2], v[q][B-1], v[q][B], v[q][B+1] (columns mod nx): E[(b ny + q) 4 + 0..3], so four
+// consecutive rows share a line.  The fused kernel writes the edge arrays of its two outputs;
+// other producers of update entries run edge_gather_launch.
+constexpr int kEdgeW = 256;
+inline int64_t edge_groups(int64_t nx) { return (nx + kEdgeW - 1) / kEdgeW; }
+inline int64_t edge_elems(int64_t ny, int64_t nx) { return edge_groups(nx) * ny * 4; }
+hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx, hipStream_t s);
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;
   int nv = 0;                      // basis vectors V_0..V_{nv-1}
@@ -134,6 +146,11 @@ struct ArnoldiArgs {
   SHCoef k{};
   double* out_v = nullptr;         // must not alias w or any V_i
   double* out_w = nullptr;
+  // edge arrays of V_0..V_{nv-1} (E[i]) and w (E[nv]); E[0] == nullptr: block halos read from
+  // the vectors themselves
+  const double* E[kArnMaxNV + 1] = {};
+  double* Eout_v = nullptr;        // edge arrays of out_v / out_w, written when non-null
+  double* Eout_w = nullptr;
   // row slab (one of several): u on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
   // arnoldi_edge_launch on every rank + the halo exchange); nullptr = single periodic slab
   const double* yh = nullptr;

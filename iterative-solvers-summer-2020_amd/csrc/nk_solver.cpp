@@ -16,7 +16,9 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 namespace nk {
 
@@ -24,6 +26,26 @@ namespace {
 constexpr double kEps = DBL_EPSILON;
 constexpr int kReduceSlots = Engine::kSlots;
 }  // namespace
+
+const char* kind_name(int kind) {
+  static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
+                                         "krylov_mdot", "krylov_combo", "reduce_final", "copy",
+                                         "halo", "user_F", "axpby", "arnoldi_fused",
+                                         "arnoldi_edge", "edge_gather"};
+  return (kind >= 0 && kind < K_NKINDS) ? names[kind] : "?";
+}
+
+void log_launch(int kind, double bytes) {
+  static std::FILE* f = [] {
+    const char* p = std::getenv("NKHIP_LAUNCH_LOG");
+    return (p && *p) ? std::fopen(p, "w") : nullptr;
+  }();
+  if (!f) return;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  std::fprintf(f, "%s %.0f\n", kind_name(kind), bytes);
+  std::fflush(f);
+}
 
 nk_opts default_opts() {
   nk_opts o;
@@ -71,6 +93,7 @@ Engine::~Engine() {
   }
   for (auto e : free_ev_) hipEventDestroy(e);
   if (own_pool_ && pool_) hipFree(pool_);
+  if (epool_) hipFree(epool_);
   if (partial_) hipFree(partial_);
   if (dres_) hipFree(dres_);
   if (hres_) hipHostFree(hres_);
@@ -94,7 +117,32 @@ int Engine::alloc(int count, std::vector<double*>* out, void* external, int64_t 
   if (hipMemsetAsync(pool_, 0, bytes, s) != hipSuccess) return NK_EHIP;
   out->resize(count);
   for (int i = 0; i < count; ++i) (*out)[i] = pool_ + npad * i;
+  pool_count_ = count;
+  if (edge_ny_ > 0 && edge_nx_ > 0) {
+    edge_n_ = edge_elems(edge_ny_, edge_nx_);
+    const int64_t eb = sizeof(double) * edge_n_ * count;
+    if (hipMalloc(reinterpret_cast<void**>(&epool_), eb) != hipSuccess) {
+      epool_ = nullptr;
+      return NK_ENOMEM;
+    }
+    bytes_ += eb;
+    if (hipMemsetAsync(epool_, 0, eb, s) != hipSuccess) return NK_EHIP;
+  }
   return NK_OK;
+}
+
+double* Engine::edges(const double* v) const {
+  if (!epool_ || !v || v < pool_) return nullptr;
+  const int64_t off = v - pool_;
+  if (off % npad != 0 || off / npad >= pool_count_) return nullptr;
+  return epool_ + edge_n_ * (off / npad);
+}
+
+int Engine::gather_edges(const double* v) {
+  double* e = edges(v);
+  if (!e) return NK_OK;
+  return launch(K_EDGE, 8.0 * edge_n_ * 2,
+                [&] { return edge_gather_launch(v, e, edge_ny_, edge_nx_, s); });
 }
 
 hipEvent_t Engine::ev() {
@@ -372,6 +420,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
   if (!rc) rc = P_.set_x0(X_);
   double red[3];
   if (!rc) rc = P_.eval(X_, X_, 0.0, nullptr, Fx_, G0_, red);
+  if (!rc) rc = P_.publish_edges(Fx_);  // V_0 of every Arnoldi process of this iterate
   if (rc) return rc;
   st_->nfev = 1;
   fx_norm_ = std::sqrt(red[0]);
@@ -414,6 +463,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
     std::swap(Fx_, Ft_);
     std::swap(G0_, Gt_);
     rc = P_.set_x0(X_);
+    if (!rc) rc = P_.publish_edges(Fx_);
     if (rc) break;
     omega_ = rdiff_ * std::max(1.0, xmax) / std::max(1.0, fmax);  // jacobian.update
     const double eta_A = gamma * fnorm_new * fnorm_new / (fx_norm_ * fx_norm_);

@@ -39,8 +39,16 @@ enum Kind : int {
   K_AXPBY,
   K_ARNOLDI,
   K_ARN_EDGE,
+  K_EDGE,
   K_NKINDS
 };
+
+// Short class name of a launch kind (the names nk_sh_kernel_profile reports).
+const char* kind_name(int kind);
+// NKHIP_LAUNCH_LOG=<path>: every Engine launch appends "<class> <algorithmic bytes>" to <path>,
+// in launch order, so a profiler's per-dispatch counters can be matched to the solver's
+// algorithmic bytes one dispatch at a time (scripts/traffic_match.py).
+void log_launch(int kind, double bytes);
 
 struct KStat {
   int64_t launches = 0;  // all launches of the class
@@ -60,8 +68,18 @@ class Engine {
   Engine& operator=(const Engine&) = delete;
 
   // Allocate `count` zeroed vectors of npad doubles from one pool (or carve from `external`).
+  // With enable_edges() called first, every pool vector also gets an edge array (edges()).
   int alloc(int count, std::vector<double*>* out, void* external = nullptr,
             int64_t external_bytes = 0);
+  // Edge arrays (nk_kernels.h, kEdgeW) of an ny x nx grid for the pool vectors.
+  void enable_edges(int64_t ny, int64_t nx) {
+    edge_ny_ = ny;
+    edge_nx_ = nx;
+  }
+  // The edge array of pool vector v (nullptr when v is not a pool vector or edges are off).
+  double* edges(const double* v) const;
+  // Refresh the edge array of pool vector v from v (no-op without one).
+  int gather_edges(const double* v);
   // Vector stride in the pool.  Large vectors get an odd multiple of 128 KiB: consecutive basis
   // vectors read at the same offset then spread over the HBM channels instead of landing on the
   // same ones (scripts/micro/march_bench.hip, 24 vectors of 4096^2 streamed row by row: pool
@@ -107,6 +125,9 @@ class Engine {
   hipEvent_t ev();
   double* pool_ = nullptr;
   bool own_pool_ = false;
+  int pool_count_ = 0;
+  double* epool_ = nullptr;
+  int64_t edge_ny_ = 0, edge_nx_ = 0, edge_n_ = 0;
   double* partial_ = nullptr;
   int64_t partial_cap_ = 0;
   double* dres_ = nullptr;
@@ -139,6 +160,7 @@ int Engine::launch(int kind, double bytes, L&& fn) {
   }
   stats_[kind].launches += 1;
   stats_[kind].bytes += bytes;
+  log_launch(kind, bytes);
   return e == hipSuccess ? NK_OK : NK_EHIP;
 }
 
@@ -173,6 +195,8 @@ struct Problem {
                          double* /*out_v*/, double* /*out_w*/, int64_t* /*nwaves*/) {
     return NK_EINVAL;
   }
+  // v (a pool vector) may enter the update of a later fused step: refresh its edge array
+  virtual int publish_edges(const double* /*v*/) { return NK_OK; }
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
 };

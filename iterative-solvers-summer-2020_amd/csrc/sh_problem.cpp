@@ -11,6 +11,8 @@ namespace nk {
 // ============================================================================================
 SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoef c, int jvp_mode)
     : E_(E), ny_(ny), nx_(nx), ny_g_(ny_global), c_(c), jvp_mode_(jvp_mode) {
+  // edge arrays for the fused Arnoldi kernel's block halos (1/64 of each pool vector)
+  if (arnoldi_supported(1, ny, nx)) E_.enable_edges(ny, nx);
   if (hipMalloc(reinterpret_cast<void**>(&B_), sizeof(double) * Engine::pad(ny * nx)) !=
       hipSuccess) {
     B_ = nullptr;
@@ -260,9 +262,22 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     if (rc) return NK_ECOMM;
     A.yh = yh_;
   }
+  // block halos from the entries' edge arrays when every entry has one (else from the vectors)
+  bool all = true;
+  for (int i = 0; i < nv; ++i) all = all && (A.E[i] = E_.edges(V[i])) != nullptr;
+  all = all && (A.E[nv] = E_.edges(w)) != nullptr;
+  if (!all || std::getenv("NKHIP_EDGES") && std::getenv("NKHIP_EDGES")[0] == '0')
+    for (int i = 0; i <= nv; ++i) A.E[i] = nullptr;
+  A.Eout_v = E_.edges(out_v);
+  A.Eout_w = E_.edges(out_w);
   // algorithmic bytes: read V (nv), w, x0 (, z); write v, w'
   const double bytes = 8.0 * double(ny_ * nx_) * (nv + 4 + (z ? 1 : 0));
   return E_.launch(K_ARNOLDI, bytes, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+}
+
+int SHProblem::publish_edges(const double* v) {
+  if (!has_fused(1)) return NK_OK;
+  return E_.gather_edges(v);
 }
 
 // ============================================================================================

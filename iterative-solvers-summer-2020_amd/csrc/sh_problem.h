@@ -30,6 +30,7 @@ class SHProblem final : public Problem {
                  double* out_v, double* out_w, int64_t* nwaves) override;
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
+  int publish_edges(const double* v) override;
 
  private:
   // any communicator (also a world of one: its halo is the periodic wrap through RCCL)

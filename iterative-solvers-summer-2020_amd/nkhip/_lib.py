@@ -83,6 +83,11 @@ SIGNATURES = [
     ("nk_sh_arnoldi_fused", C.c_int, [C.POINTER(_P), C.POINTER(_D), _I32, _P, _D, _P, _P, _P,
                                       _I64, _I64, _D, _D, _D, _D, _D, _D, _P, _P,
                                       C.POINTER(_D), _P]),
+    ("nk_edge_elems", C.c_int64, [_I64, _I64]),
+    ("nk_edge_gather", C.c_int, [_P, _P, _I64, _I64, _P]),
+    ("nk_sh_arnoldi_fused_edges", C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_D), _I32,
+                                            _P, _D, _P, _P, _P, _I64, _I64, _D, _D, _D, _D, _D,
+                                            _D, _P, _P, _P, _P, C.POINTER(_D), _P]),
     ("nk_dot", C.c_int, [_P, _P, _I64, C.POINTER(_D), _P]),
     ("nk_nrm2", C.c_int, [_P, _I64, C.POINTER(_D), _P]),
     ("nk_maxnorm", C.c_int, [_P, _I64, C.POINTER(_D), _P]),

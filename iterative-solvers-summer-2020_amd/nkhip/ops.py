@@ -97,13 +97,15 @@ def sh_fdjvp(x0, G0, z, h, r, k, g, zs, sc, ny=None, nx=None, out=None):
 
 
 def sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=None, ny=None, nx=None,
-                     v_out=None, w_out=None, reduce=True):
+                     v_out=None, w_out=None, reduce=True, E=None, Ev_out=None, Ew_out=None):
     """One fused Arnoldi step (csrc/arnoldi.hip): the Gram-Schmidt update of scipy's _fgmres
     (_gcrotmk.py:104-143) ``v = tau*w + sum_i coef[i]*V[i]``, the next FD matvec
     (_nonlin.py:1500-1513) ``w' = (G(x0 + sc*zs*z) - G(x0))/sc`` with ``z = v`` unless given, and
     the next multi-dot, all in one pass over the basis.  Returns ``(v, w', dots)`` with
     ``dots = [w'.V_i..., w'.v, v.V_i..., v.v, w'.w']`` (None when ``reduce`` is False).  The
-    difference quotient is evaluated in closed form, so ``G0`` is not read (it may be None)."""
+    difference quotient is evaluated in closed form, so ``G0`` is not read (it may be None).
+    ``E`` (optional): the edge arrays (``edge_gather``) of V[0..nv-1] and w, from which the block
+    halos are then read; ``Ev_out`` / ``Ew_out`` receive the edge arrays of v and w'."""
     for t, nm in ((w, "w"), (x0, "x0")):
         _dev(t, nm)
     ny, nx = _grid(x0, ny, nx)
@@ -114,12 +116,31 @@ def sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=None, ny=Non
     w_out = torch.empty_like(x0) if w_out is None else _dev(w_out, "w_out")
     dots = (C.c_double * (2 * nv + 3))() if reduce else None
     zp = _ptr(_dev(z, "z")) if z is not None else None
-    check(lib.nk_sh_arnoldi_fused(ptrs, cf, nv, _ptr(w), float(tau), _ptr(x0),
-                                  _ptr(G0) if G0 is not None else None, zp, ny,
-                                  nx, float(h), float(r), float(k), float(g), float(zs),
-                                  float(sc), _ptr(v_out), _ptr(w_out), dots, _stream()),
-          "nk_sh_arnoldi_fused")
+    common = (cf, nv, _ptr(w), float(tau), _ptr(x0), _ptr(G0) if G0 is not None else None, zp,
+              ny, nx, float(h), float(r), float(k), float(g), float(zs), float(sc), _ptr(v_out),
+              _ptr(w_out))
+    if E is None:
+        check(lib.nk_sh_arnoldi_fused(ptrs, *common, dots, _stream()), "nk_sh_arnoldi_fused")
+    else:
+        if len(E) != nv + 1:
+            raise ValueError("E holds the edge arrays of V[0..nv-1] and w")
+        eptrs = (C.c_void_p * (nv + 1))(*[_dev(e, "E[i]").data_ptr() for e in E])
+        check(lib.nk_sh_arnoldi_fused_edges(
+            ptrs, eptrs, *common, _ptr(Ev_out) if Ev_out is not None else None,
+            _ptr(Ew_out) if Ew_out is not None else None, dots, _stream()),
+            "nk_sh_arnoldi_fused_edges")
     return v_out, w_out, (list(dots) if reduce else None)
+
+
+def edge_gather(v, ny=None, nx=None, out=None):
+    """The edge array of grid vector v (nkhip.h, nk_edge_gather): the two columns either side of
+    every 256-column group boundary, four values per boundary and row."""
+    _dev(v, "v")
+    ny, nx = _grid(v, ny, nx)
+    n = int(lib.nk_edge_elems(ny, nx))
+    out = torch.empty(n, dtype=torch.float64, device=v.device) if out is None else out
+    check(lib.nk_edge_gather(_ptr(v), _ptr(out), ny, nx, _stream()), "nk_edge_gather")
+    return out
 
 
 def dot(x, y) -> float:

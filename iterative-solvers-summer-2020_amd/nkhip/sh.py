@@ -142,8 +142,8 @@ class SwiftHohenberg:
 
     # ----------------------------------------------------------------------------- profiling
     def kernel_profile(self):
-        recs = (_lib.nk_kprof * 16)()
-        n = check(lib.nk_sh_kernel_profile(self._h, recs, 16), "nk_sh_kernel_profile")
+        recs = (_lib.nk_kprof * 32)()
+        n = check(lib.nk_sh_kernel_profile(self._h, recs, 32), "nk_sh_kernel_profile")
         return {recs[i].name.decode(): {"launches": recs[i].launches, "ms": recs[i].total_ms,
                                         "alg_bytes": recs[i].alg_bytes, "timed": recs[i].timed,
                                         "timed_bytes": recs[i].timed_bytes} for i in range(n)}

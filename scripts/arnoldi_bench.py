@@ -24,12 +24,19 @@ def main():
     w, x0, z, G0 = (torch.randn(N, N, dtype=torch.float64, device="cuda") for _ in range(4))
     vo = torch.empty_like(w)
     wo = torch.empty_like(w)
+    # ARN_EDGES=1: block halos from edge arrays (the solver's default), the outputs' written
+    edges = os.environ.get("ARN_EDGES", "1") == "1"
+    EV = [nkhip.edge_gather(t) for t in V] if edges else None
+    Ew = nkhip.edge_gather(w) if edges else None
+    Evo, Ewo = (torch.empty_like(Ew), torch.empty_like(Ew)) if edges else (None, None)
     out = []
     for ext in (False, True):
         for nv in nvs:
             coef = [0.01] * nv
             args = (V[:nv], coef, w, 1.0, x0, G0, 0.625, 0.01, 0.2, 1.0, 1.0, 1e-7)
             kw = dict(z=z if ext else None, v_out=vo, w_out=wo, reduce=False)
+            if edges:
+                kw.update(E=EV[:nv] + [Ew], Ev_out=Evo, Ew_out=Ewo)
             for _ in range(3):
                 nkhip.sh_arnoldi_fused(*args, **kw)
             torch.cuda.synchronize()

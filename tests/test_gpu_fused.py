@@ -157,3 +157,40 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx):
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
     F = sh_oracle.residual(got.reshape(-1), U0.reshape(-1), ny_total, nx, 0.625, 0.01, 0.2, 1.0)
     assert np.abs(F).max() <= 1e-9
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 64), (40, 130), (24, 600), (16, 4), (8, 512)])
+@pytest.mark.parametrize("ext", [False, True])
+def test_fused_kernel_edges_identical(ny, nx, ext):
+    """Block halos read from the entries' edge arrays (nk_sh_arnoldi_fused_edges) are the same
+    values as read from the vectors: v, w' and every dot product are bitwise equal, and the edge
+    arrays the kernel writes for v and w' equal nk_edge_gather of the outputs."""
+    import nkhip
+    nv = 7
+    gen = torch.Generator(device="cpu").manual_seed(nx + ny)
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    V = [rnd() for _ in range(nv)]
+    coef = [float(c) for c in torch.randn(nv, generator=gen, dtype=torch.float64)]
+    w, x0 = rnd(), rnd()
+    z = rnd() if ext else None
+    args = (V, coef, w, 0.75, x0, None, 0.625, 0.01, 0.2, 1.0, 0.5, 1e-3)
+    v1, w1, d1 = nkhip.sh_arnoldi_fused(*args, z=z)
+    E = [nkhip.edge_gather(t) for t in V + [w]]
+    Ev = torch.full_like(E[0], float("nan"))
+    Ew = torch.full_like(E[0], float("nan"))
+    v2, w2, d2 = nkhip.sh_arnoldi_fused(*args, z=z, E=E, Ev_out=Ev, Ew_out=Ew)
+    assert torch.equal(v1, v2) and torch.equal(w1, w2) and d1 == d2
+    assert torch.equal(Ev, nkhip.edge_gather(v2))
+    assert torch.equal(Ew, nkhip.edge_gather(w2))
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 600), (128, 512)])
+def test_edges_identical_solve(ny, nx, monkeypatch):
+    """The solver with edge arrays (default) and without (NKHIP_EDGES=0) is bitwise the same;
+    the edge arrays were used (edge_gather launches for the non-fused producers)."""
+    monkeypatch.setenv("NKHIP_EDGES", "0")
+    _, a, sa, pa = _step(ny, nx, fused=True)
+    monkeypatch.delenv("NKHIP_EDGES")
+    _, b, sb, pb = _step(ny, nx, fused=True)
+    assert np.array_equal(a, b) and sa == sb
+    assert pb["edge_gather"]["launches"] > 0 and pb["arnoldi_fused"]["launches"] > 0
