@@ -310,6 +310,10 @@ def main():
     comm = None
     if world > 1 or args.rccl_self:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:  # --rccl-self without a launcher: a world of one
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         comm = nkhip.RcclComm.from_torch_distributed()
 

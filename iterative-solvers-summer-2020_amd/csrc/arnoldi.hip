@@ -194,8 +194,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const int hh = lane & 3;
   const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WPB * kSW - 2 + hh;
   const int64_t hcol = ((hc % nx) + nx) % nx;
-  const int64_t r0 = band * A.RY;
-  const int64_t r1 = (r0 + A.RY < ny) ? r0 + A.RY : ny;
+  const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
+  const int64_t r0 = A.r_begin + band * A.RY;
+  const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
   const int64_t nrows = r1 - r0;
   const SHCoef& K = A.k;
   const double isc = 1.0 / A.sc;
@@ -538,8 +539,8 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   double t3[3] = {awn, avv, aww};
   wave_sum<3>(t3);
   if (l == 0) {
-    const int64_t nw = ngroups * WPB * A.nbands;  // every wave of every block writes a column
-    double* p = A.partial + gw;
+    const int64_t nw = A.pstride;  // every wave of every block writes a column
+    double* p = A.partial + A.pcol0 + gw;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int e = 2 * k + hf;
@@ -587,17 +588,28 @@ hipError_t launch_t(ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
   // partial columns than the caller's buffer holds
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
   const int64_t strips = (A.nx + kSW - 1) / kSW;
-  const int64_t target = int64_t(occ.ncu) * occ.blocks_per_cu * WPB * (rounds > 0 ? rounds : 1);
+  const int64_t rb = A.r_begin, re = (A.r_end >= 0) ? A.r_end : A.ny;
+  if (rb < 0 || re > A.ny || re <= rb) return hipErrorInvalidValue;
+  const int64_t rows = re - rb;
+  const int64_t ncu_use = (occ.ncu - A.reserve_cus > 0) ? occ.ncu - A.reserve_cus : 1;
+  const int64_t target = ncu_use * occ.blocks_per_cu * WPB * (rounds > 0 ? rounds : 1);
   const int64_t wpr = (strips + WPB - 1) / WPB * WPB;  // waves per band (whole blocks)
   int64_t nbands = target / wpr;
   const int64_t cap_bands = A.partial_cap / ((2 * int64_t(NV) + 3) * wpr);
   if (nbands > cap_bands) nbands = cap_bands;
-  if (nbands > A.ny / 8) nbands = A.ny / 8;
+  if (nbands > rows / 8) nbands = rows / 8;
   if (nbands < 1) nbands = 1;
-  const int64_t RY = (A.ny + nbands - 1) / nbands;
-  nbands = (A.ny + RY - 1) / RY;
+  const int64_t RY = (rows + nbands - 1) / nbands;
+  nbands = (rows + RY - 1) / RY;
   const int64_t nw = wpr * nbands;
-  if (nw * (2 * int64_t(NV) + 3) > A.partial_cap) return hipErrorInvalidValue;
+  if (A.plan_only) {
+    *nwaves = nw;
+    return hipSuccess;
+  }
+  if (A.pstride == 0) A.pstride = nw;
+  if (A.pcol0 < 0 || A.pcol0 + nw > A.pstride ||
+      A.pstride * (2 * int64_t(NV) + 3) > A.partial_cap)
+    return hipErrorInvalidValue;
   A.strips = int(strips);
   A.nbands = int(nbands);
   A.RY = int(RY);

@@ -154,8 +154,16 @@ struct ArnoldiArgs {
   // row slab (one of several): u on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
   // arnoldi_edge_launch on every rank + the halo exchange); nullptr = single periodic slab
   const double* yh = nullptr;
-  double* partial = nullptr;       // [(2 nv + 3)][nwaves]
+  double* partial = nullptr;       // [(2 nv + 3)][pstride], this launch's columns from pcol0
   int64_t partial_cap = 0;         // doubles available at partial
+  // rows [r_begin, r_end) of the slab are computed (r_end < 0: ny); rows outside are read only
+  // (a band's two halo rows on either side).  Several launches over disjoint row ranges may share
+  // one partial buffer: pstride = the total columns (0: this launch's own), pcol0 = its first.
+  int64_t r_begin = 0, r_end = -1;
+  int64_t pstride = 0, pcol0 = 0;
+  bool plan_only = false;          // set *nwaves only, launch nothing
+  int reserve_cus = 0;             // size the grid to leave this many CUs free (a concurrent
+                                   // halo exchange needs CUs for its kernels)
 };
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']

@@ -31,7 +31,7 @@ const char* kind_name(int kind) {
   static const char* names[K_NKINDS] = {"sh_fdjvp", "sh_ajvp", "sh_trial", "sh_bold",
                                          "krylov_mdot", "krylov_combo", "reduce_final", "copy",
                                          "halo", "user_F", "axpby", "arnoldi_fused",
-                                         "arnoldi_edge", "edge_gather"};
+                                         "arnoldi_edge", "edge_gather", "arnoldi_slab_edges"};
   return (kind >= 0 && kind < K_NKINDS) ? names[kind] : "?";
 }
 

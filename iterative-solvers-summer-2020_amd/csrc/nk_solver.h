@@ -40,6 +40,7 @@ enum Kind : int {
   K_ARNOLDI,
   K_ARN_EDGE,
   K_EDGE,
+  K_ARN_SLAB,
   K_NKINDS
 };
 
@@ -91,7 +92,12 @@ class Engine {
   }
 
   template <class L>
-  int launch(int kind, double bytes, L&& fn);
+  int launch(int kind, double bytes, L&& fn) {
+    return launch_on(kind, bytes, s, static_cast<L&&>(fn));
+  }
+  // The same for a launch on another stream `st` (timed with events on st).
+  template <class L>
+  int launch_on(int kind, double bytes, hipStream_t st, L&& fn);
   // Finish a reduction whose per-block partials are in partial(): values [0,nsum) summed,
   // [nsum,nv) max-reduced, across blocks and ranks; result in out[0,nv).  Synchronises.
   int reduce(int64_t nblk, int nsum, int nv, double* out);
@@ -145,17 +151,17 @@ class Engine {
 };
 
 template <class L>
-int Engine::launch(int kind, double bytes, L&& fn) {
+int Engine::launch_on(int kind, double bytes, hipStream_t st, L&& fn) {
   hipEvent_t a = nullptr, b = nullptr;
   const bool timed = profile && (tick_[kind]++ % sample == 0);
   if (timed) {
     a = ev();
-    hipEventRecord(a, s);
+    hipEventRecord(a, st);
   }
   const hipError_t e = fn();
   if (timed) {
     b = ev();
-    hipEventRecord(b, s);
+    hipEventRecord(b, st);
     pend_.push_back(Pending{kind, a, b, bytes});
   }
   stats_[kind].launches += 1;

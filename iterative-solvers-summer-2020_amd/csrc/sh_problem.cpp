@@ -250,18 +250,6 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   A.out_w = out_w;
   A.partial = E_.partial();
   A.partial_cap = E_.partial_cap();
-  if (dist()) {
-    // edge rows of u -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
-    const double eb = 8.0 * 4 * nx_ * (z ? 2 : nv + 2);
-    int rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
-    if (rc) return rc;
-    rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
-      return E_.comm->halo(y4_, yh_, yh_ + 2 * nx_, 4, nx_, E_.s) == NK_OK ? hipSuccess
-                                                                         : hipErrorUnknown;
-    });
-    if (rc) return NK_ECOMM;
-    A.yh = yh_;
-  }
   // block halos from the entries' edge arrays when every entry has one (else from the vectors)
   bool all = true;
   for (int i = 0; i < nv; ++i) all = all && (A.E[i] = E_.edges(V[i])) != nullptr;
@@ -270,9 +258,79 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     for (int i = 0; i <= nv; ++i) A.E[i] = nullptr;
   A.Eout_v = E_.edges(out_v);
   A.Eout_w = E_.edges(out_w);
-  // algorithmic bytes: read V (nv), w, x0 (, z); write v, w'
-  const double bytes = 8.0 * double(ny_ * nx_) * (nv + 4 + (z ? 1 : 0));
-  return E_.launch(K_ARNOLDI, bytes, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+  // algorithmic bytes per row: read V (nv), w, x0 (, z); write v, w'
+  const double rowb = 8.0 * double(nx_) * (nv + 4 + (z ? 1 : 0));
+  if (!dist())
+    return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+
+  // Row slab: the stencil of rows 0, 1, ny-2, ny-1 needs u on the neighbours' edge rows, which
+  // this step computes.  Every rank evaluates u on its own edge rows (a 4-row launch) and
+  // exchanges them with its ring neighbours; meanwhile the interior rows [2, ny-2), whose
+  // stencil reads only this slab's rows, run on the side stream.  The two 2-row edge bands follow
+  // the exchange.  All three launches write disjoint columns of one partial buffer, so the
+  // multi-dot stays one reduction (one all-reduce).  Opt-in (NKHIP_SLAB_OVERLAP=1): measured at
+  // world size 1 over RCCL (4096 rows, scripts/slab_ab.sh, profiles/r02_slab_overlap.md) the
+  // interior pass loses more to the CUs it leaves for the exchange kernels, plus the two
+  // latency-bound 2-row launches after it, than the exchange costs in series (0.678 vs 0.658 ms
+  // per Arnoldi step); the default is one launch after the exchange.
+  const char* ov = std::getenv("NKHIP_SLAB_OVERLAP");
+  const bool split = ny_ >= 12 && side_ && (ov && ov[0] == '1');
+  ArnoldiArgs I = A, T = A, Bm = A;
+  int64_t nwI = 0, nwT = 0, nwB = 0;
+  if (split) {
+    I.r_begin = 2;
+    I.r_end = ny_ - 2;
+    // leave CUs for the edge kernel and the RCCL send/recv kernels that run beside it (a
+    // resident round of fused blocks holds every CU until it ends)
+    static const int reserve = [] {
+      const char* e = std::getenv("NKHIP_SLAB_RESERVE_CUS");
+      return (e && *e) ? std::atoi(e) : 8;
+    }();
+    I.reserve_cus = reserve;
+    T.r_begin = 0;
+    T.r_end = 2;
+    Bm.r_begin = ny_ - 2;
+    Bm.r_end = ny_;
+    I.plan_only = T.plan_only = Bm.plan_only = true;
+    if (arnoldi_launch(I, E_.s, &nwI) != hipSuccess || arnoldi_launch(T, E_.s, &nwT) != hipSuccess ||
+        arnoldi_launch(Bm, E_.s, &nwB) != hipSuccess)
+      return NK_EHIP;
+    I.plan_only = T.plan_only = Bm.plan_only = false;
+    I.pstride = T.pstride = Bm.pstride = nwI + nwT + nwB;
+    I.pcol0 = 0;
+    T.pcol0 = nwI;
+    Bm.pcol0 = nwI + nwT;
+    if (hipEventRecord(ev_in_, E_.s) != hipSuccess || hipStreamWaitEvent(side_, ev_in_, 0) != hipSuccess)
+      return NK_EHIP;
+    int64_t nw = 0;
+    int rc = E_.launch_on(K_ARNOLDI, rowb * (ny_ - 4), side_,
+                          [&] { return arnoldi_launch(I, side_, &nw); });
+    if (rc) return rc;
+    if (hipEventRecord(ev_out_, side_) != hipSuccess) return NK_EHIP;
+  }
+  // edge rows of u -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
+  const double eb = 8.0 * 4 * nx_ * (z ? 2 : nv + 2);
+  int rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
+  if (rc) return rc;
+  rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
+    return E_.comm->halo(y4_, yh_, yh_ + 2 * nx_, 4, nx_, E_.s) == NK_OK ? hipSuccess
+                                                                       : hipErrorUnknown;
+  });
+  if (rc) return NK_ECOMM;
+  if (!split) {
+    A.yh = yh_;
+    return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+  }
+  T.yh = Bm.yh = yh_;
+  int64_t nw = 0;
+  rc = E_.launch(K_ARN_SLAB, rowb * 4, [&] {
+    hipError_t e = arnoldi_launch(T, E_.s, &nw);
+    if (e == hipSuccess) e = arnoldi_launch(Bm, E_.s, &nw);
+    if (e == hipSuccess) e = hipStreamWaitEvent(E_.s, ev_out_, 0);
+    return e;
+  });
+  *nwaves = nwI + nwT + nwB;
+  return rc;
 }
 
 int SHProblem::publish_edges(const double* v) {

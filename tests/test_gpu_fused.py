@@ -119,14 +119,17 @@ def test_fused_kernel_vs_torch(ny, nx, nv, ext):
         assert abs(a - b) <= 1e-10 * scale, (i, a, b)
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("nranks,ny_total,nx", [(2, 64, 64), (3, 96, 130), (4, 48, 40),
                                                   (8, 1024, 1024)])
-def test_fused_slabs_match_single_slab(nranks, ny_total, nx):
+def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, monkeypatch):
     """Row slabs through the fused kernel: every rank evaluates y on its edge rows, the loopback
     communicator exchanges them (the RCCL path's protocol), and the fused pass takes them as its
     halo rows.  Same root as the single periodic slab, and the fused kernel did run on each slab."""
     import nkhip
     from conftest import run_slabs
+    # "1": interior rows on a side stream during the edge exchange, edge bands after it
+    monkeypatch.setenv("NKHIP_SLAB_OVERLAP", overlap)
     U0 = np.random.default_rng(7).standard_normal((ny_total, nx))
     single = nkhip.SwiftHohenberg(N=nx, ny=ny_total, d=0.625 * nx, f_tol=1e-10)
     ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
@@ -152,6 +155,8 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx):
     for pr in profs:
         assert pr["arnoldi_fused"]["launches"] > 0
         assert pr["arnoldi_edge"]["launches"] == pr["arnoldi_fused"]["launches"]
+        if overlap == "1" and ny_total // nranks >= 12:
+            assert pr["arnoldi_slab_edges"]["launches"] == pr["arnoldi_fused"]["launches"]
     assert len(set(nits)) == 1 and abs(nits[0] - ref_nit) <= 1
     got = np.concatenate(out, axis=0)
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
