@@ -222,7 +222,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
         st_->n_arnoldi += 1;
         const int np1 = j + 2;
         rc = E_.reduce_async(nw, 2 * np1 + 1, 2 * np1 + 1, Engine::kSlotMdot);
-        if (!rc) rc = E_.sync();
+        if (!rc) rc = E_.wait_results(Engine::kSlotMdot, 2 * np1 + 1);
         if (rc) return rc;
         hn_pending = true;
         ++j;

@@ -13,6 +13,7 @@
 #include "nk_solver.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -187,10 +188,41 @@ int Engine::copy(double* dst, const double* src, int64_t cnt) {
   });
 }
 
+namespace {
+// a signalling-NaN bit pattern no reduction of finite or NaN data writes (NaNs a reduction
+// propagates are quiet): marks a pinned result slot as not yet written
+constexpr uint64_t kUnset = 0x7FF0DEADBEEF0001ull;
+bool poll_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NKHIP_POLL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
+int Engine::wait_results(int slot, int nv) {
+  if (comm || !poll_enabled()) return sync();
+  volatile uint64_t* h = reinterpret_cast<volatile uint64_t*>(hres_ + slot);
+  for (int k = 0; k < nv; ++k) {
+    for (int64_t spins = 0; h[k] == kUnset; ++spins) {
+      if (spins > (int64_t(1) << 26)) return sync();  // not arriving: take the slow path
+      __builtin_ia32_pause();
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return NK_OK;
+}
+
 int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot) {
   if (slot < 0 || slot + nv > kReduceSlots) return NK_EINVAL;
   // any communicator (also a world of one) takes the all-reduce path
   const bool multi = comm != nullptr;
+  if (!multi) {  // the kernel fills these pinned slots; wait_results() polls for them
+    uint64_t* h = reinterpret_cast<uint64_t*>(hres_ + slot);
+    for (int k = 0; k < nv; ++k) h[k] = kUnset;
+    std::atomic_thread_fence(std::memory_order_release);
+  }
   int rc = launch(K_REDUCE, 8.0 * nblk * nv, [&] {
     return reduce_final_launch(partial_, nblk, nsum, nv, dres_ + slot,
                                multi ? nullptr : hres_ + slot, s);

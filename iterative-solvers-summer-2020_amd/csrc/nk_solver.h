@@ -111,6 +111,11 @@ class Engine {
   static constexpr int kSlotCombo = 256;  // 2 values
   static constexpr int kSlotSync = 384;   // reduce()
   int sync();
+  // Wait for the nv results a reduce_async(.., slot) writes to the pinned host slots, by polling
+  // them (the reduction kernel stores every value straight into pinned memory, the slots were
+  // marked beforehand); no stream synchronisation.  Falls back to sync() with a communicator
+  // (results come through a D2H copy), after ~1 s, or with NKHIP_POLL=0.
+  int wait_results(int slot, int nv);
   int copy(double* dst, const double* src, int64_t n);
 
   double* partial() const { return partial_; }
