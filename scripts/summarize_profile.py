@@ -52,7 +52,7 @@ def main():
                 bench = json.loads(line)
     out = [f"# rocprofv3 summary `{tag}`", "",
            "Command: `scripts/profile.sh` = `rocprofv3 --kernel-trace --stats` over "
-           "`python3 bench.py " + (" ".join(sys.argv[2:]) or "--steps 3 --warmup 0 --cpu-baseline off")
+           "`python3 bench.py " + (" ".join(sys.argv[2:]) or "--steps 3 --warmup 1 --cpu-baseline off --extra off")
            + "`, then two separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes.", "",
            "| kernel | calls | avg us (rocprof) | % time | HBM read MB/launch (2x FETCH_SIZE) "
            "| HBM write MB/launch |", "|---|---|---|---|---|---|"]
@@ -71,51 +71,21 @@ def main():
                                        if k in bench}, indent=1), "```"]
     open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w").write("\n".join(out) + "\n")
     print("\n".join(out))
-    # per-kernel-class HBM traffic per launch (PMC) next to the algorithmic bytes of the SAME run;
-    # a class sums every instantiation of its kernel template (arnoldi_kernel<nv, ext, pf, nt>)
-    def klass(k):
-        if k.startswith("arnoldi_kernel<"):
-            return "arnoldi_fused"
-        if k.startswith("arnoldi_edge_kernel"):
-            return "arnoldi_edge"
-        if k.startswith("combo_kernel<"):
-            return "krylov_combo"
-        if k.startswith("mdot_kernel<"):
-            return "krylov_mdot"
-        if k.startswith("reduce_final_kernel"):
-            return "reduce_final"
-        for mode, cls in (("5", "sh_fdjvp"), ("6", "sh_ajvp"), ("4", "sh_trial"), ("3", "sh_bold")):
-            if k.startswith(f"march_kernel<(nk::SMode){mode},"):
-                return cls
-        return None
-
-    def by_class(agg):
-        out = collections.defaultdict(lambda: [0, 0.0])
-        for k, (n, v) in agg.items():
-            c = klass(k)
-            if c:
-                out[c][0] += n
-                out[c][1] += v
-        return out
-
-    fc, wc = by_class(fetch), by_class(write)
-    traffic = {"tag": tag, "source": f"profiles/{tag}_summary.md", "classes": {}}
-    for cls in sorted(fc):
-        f, w = fc[cls], wc.get(cls)
-        if not w or not f[0] or not w[0]:
-            continue
-        rec = {"launches": f[0], "hbm_read_bytes_per_launch": 2 * f[1] * 1024 / f[0],
-               "hbm_write_bytes_per_launch": w[1] * 1024 / w[0]}
-        if bench and cls in bench.get("kernels", {}):
-            kb = bench["kernels"][cls]
-            alg = (kb["alg_MB_per_launch"] * 1e6 if "alg_MB_per_launch" in kb
-                   else kb["GB/s"] * 1e9 * kb["ms"] * 1e-3 / kb["launches"])
-            rec["alg_bytes_per_launch"] = alg
-            rec["traffic_over_alg"] = (rec["hbm_read_bytes_per_launch"]
-                                       + rec["hbm_write_bytes_per_launch"]) / alg
-        traffic["classes"][cls] = rec
-    for name in (f"{tag}_traffic.json", "latest_traffic.json"):
-        json.dump(traffic, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
+    # per-kernel-class traffic: the per-dispatch match (scripts/traffic_match.py) of the same run
+    tj = os.path.join(ROOT, "profiles", f"{tag}_traffic.json")
+    if os.path.exists(tj):
+        t = json.load(open(tj))
+        extra = ["", "Per-dispatch HBM traffic against algorithmic bytes (`" + os.path.basename(tj)
+                 + "`, " + t["source"] + "):", "",
+                 "| class | dispatches | traffic / algorithmic | per-dispatch min..max | avg us | "
+                 "algorithmic GB/s |", "|---|---|---|---|---|---|"]
+        for c, v in sorted(t["classes"].items()):
+            extra.append(f"| {c} | {v['dispatches_matched']} | {v['traffic_over_alg']:.4f} | "
+                         f"{v['per_dispatch_ratio_min']:.3f}..{v['per_dispatch_ratio_max']:.3f} | "
+                         f"{v.get('avg_us', 0):.1f} | {v.get('alg_GBps', 0):.0f} |")
+        with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "a") as fh:
+            fh.write("\n".join(extra) + "\n")
+        print("\n".join(extra))
 
 
 if __name__ == "__main__":
