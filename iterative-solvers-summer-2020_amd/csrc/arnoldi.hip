@@ -557,6 +557,303 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Wide layout (basis lengths up to kWideMaxNV): a wave owns 128 aligned columns, every lane holds
+// columns 2l, 2l+1 of ALL entries, so each load instruction streams one 1-KB row segment of one
+// vector (the vector-pair layout streams two 512-B segments: 0.69 against 0.73 of 8 TB/s for the
+// bare pattern, scripts/micro/pattern2_bench.hip) and a block of W waves owns 128 W columns (W = 4:
+// half the block-halo lines per column of the pair layout, whose halo costs ~9 % of a launch,
+// profiles/r02_arnoldi_ab.md).  The LDS lag holds every basis entry of two rows for the W*128
+// columns, 16 (nv+1) W KB: 152 KB at nv = 18, W = 4 -- which is what bounds this layout to short
+// bases.  The update sum runs over the entries in order (arnoldi_edge_kernel matches it).
+constexpr int kWW = 128;       // columns per wave
+constexpr int kWideMaxNV = 18;  // LDS: 2 rows x (nv + 1) x 4 waves x 1 KB <= 152 KB
+
+template <int NV, bool EXT, int PF, bool NT, int W>
+__global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs A) {
+  constexpr int RR = PF + 1;
+  constexpr int NE = NV + 2 + (EXT ? 1 : 0);  // [V_0 .. V_{NV-1}, w, x0, (z)]
+  constexpr int EX = NV + 1, EZ = NV + 2;
+  static_assert(NV + 1 <= 16 * W, "one packed halo load per row");
+  __shared__ dv2 lag[W][2][NV + 1][64];  // basis rows r, r+1 and x0 (slot NV)
+  __shared__ double edge[2][W][4];
+  __shared__ double hpart[2][W][4];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = blockIdx.x;
+  const int64_t bpx = gridDim.x / 8;  // XCD-aware: each XCD gets a contiguous run of blocks
+  const int64_t L = (b % 8) * bpx + b / 8;
+  const int64_t ngroups = (A.strips + W - 1) / W;
+  if (L >= ngroups * A.nbands) return;
+  const int64_t band = L / ngroups, grp = L % ngroups;
+  const int64_t gw = L * W + wid;
+  const int64_t nx = A.nx, ny = A.ny;
+  const int64_t B0 = grp * W * kWW;
+  const int64_t c = B0 + wid * kWW + 2 * lane;
+  const int64_t col = c % nx;
+  const bool own = c < nx;
+  const int hh = lane & 3;  // block halo: columns B0-2, B0-1, B0 + 128 W, +1
+  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + W * kWW - 2 + hh;
+  const int64_t hcol = ((hc % nx) + nx) % nx;
+  const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
+  const int64_t r0 = A.r_begin + band * A.RY;
+  const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
+  const int64_t nrows = r1 - r0;
+  const SHCoef& K = A.k;
+  const double isc = 1.0 / A.sc;
+  const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
+  dv2 (*lg)[NV + 1][64] = lag[wid];
+  auto src = [&](int e) -> const double* {
+    if (e < NV) return A.V[e];
+    if (e == NV) return A.w;
+    if (e == EX) return A.x0;
+    return A.z;
+  };
+  auto cof = [&](int e) -> double { return e < NV ? A.c[e] : A.tau; };  // e <= NV
+  // packed block-halo loads: lane 4e' + hh of wave w fetches column hh of entry w + W e'
+  const double *hp, *hE;
+  double hcf;
+  {
+    const int e = wid + W * (lane >> 2);
+    const double* p = A.w;
+    const double* pe = A.E[NV];
+    double cf = 0.0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      p = (e == j) ? A.V[j] : p;
+      pe = (e == j) ? A.E[j] : pe;
+      cf = (e == j) ? A.c[j] : cf;
+    }
+    cf = (e == NV) ? A.tau : cf;
+    hp = p;
+    hE = pe;
+    hcf = cf;
+  }
+  const bool useE = A.E[0] != nullptr;
+  const int64_t nbE = edge_groups(nx);
+  const int64_t bL = B0 / kEdgeW, bR = ((B0 + W * kWW) / kEdgeW) % nbE;
+  const bool eL = own && (c % kEdgeW == 0);
+  const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
+  const int64_t ebo =
+      eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
+  const bool eOn = eL || eR;
+  const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
+  auto eoff = [&](int64_t q) -> uint32_t {
+    return eOn ? uint32_t(((ebo / 4) * ny * 4 + q * 4 + (ebo & 3)) * 8) : kOOB;
+  };
+  const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
+  const bool slab = A.yh != nullptr;
+  const double* yhb = slab ? A.yh : A.x0;
+  auto wrap = [&](int64_t q) -> int64_t {
+    q = (q > r1 + 1) ? r1 + 1 : q;
+    return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
+  };
+
+  struct Slot {
+    dv2 e[NE];
+    double hv, hx;
+    bool own;
+  };
+  auto load = [&](Slot& s, int64_t q) {
+    const int64_t qq = wrap(q);
+    const int64_t o = qq * nx + col;
+    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
+    const bool hrow = slab && (qc < 0 || qc >= ny);
+    const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const double* a = src(e) + o;
+      if (e == EX) a = hrow ? yhb + hq * nx + col : a;
+      const dv2* p = reinterpret_cast<const dv2*>(a);
+      if constexpr (NT)
+        s.e[e] = __builtin_nontemporal_load(p);
+      else
+        s.e[e] = *p;
+    }
+    const int64_t ho = qq * nx + hcol;
+    const int64_t eo = ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh;
+    if constexpr (!EXT) s.hv = *(useE ? hE + eo : hp + ho);
+    s.hx = *((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
+    s.own = !hrow;
+  };
+  auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
+    dv2 (*d)[64] = lg[(q - r0) & 1];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) d[e][lane] = s.e[e];
+    d[NV][lane] = g;
+  };
+
+  dv2 yw[5], hw[5], vw[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
+  dv2 gq{0.0, 0.0};
+  auto push = [&](const Slot& s, int64_t q) {
+    dv2 v{0.0, 0.0};
+#pragma unroll
+    for (int e = 0; e <= NV; ++e) {  // entry order (the slab edge kernel sums the same way)
+      v.x += cof(e) * s.e[e].x;
+      v.y += cof(e) * s.e[e].y;
+    }
+    const dv2 xe = s.e[EX];
+    gq = xe;
+    dv2 u;
+    if constexpr (EXT)
+      u = s.own ? s.e[EZ] : xe;
+    else
+      u = s.own ? v : xe;
+    const int slot = int(q & 1);
+    if constexpr (!EXT) {
+      double hs = hcf * s.hv;
+      hs += dpp_row_shr(hs, 4);
+      hs += dpp_row_shr(hs, 8);
+      hs = pair16_sum(hs);
+      hs = pair_sum(hs);
+      if ((lane & ~3) == 12) hpart[slot][wid][lane & 3] = hs;
+    }
+    if (lane == 0) {
+      edge[slot][wid][0] = u.x;
+      edge[slot][wid][1] = u.y;
+    }
+    if (lane == 63) {
+      edge[slot][wid][2] = u.x;
+      edge[slot][wid][3] = u.y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    double hz = 0.0;
+    if constexpr (EXT) {
+      hz = __shfl(s.hx, hh + 4, 64);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) hz += hpart[slot][w][hh];
+    }
+    const double yh = s.own ? hz : s.hx;
+    const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < W - 1) ? wid + 1 : W - 1;
+    const double el2 = edge[slot][wl][2], el1 = edge[slot][wl][3];
+    const double er1 = edge[slot][wr][0], er2 = edge[slot][wr][1];
+    const double hl2 = readlane(yh, 0), hl1 = readlane(yh, 1);
+    const double hr1 = readlane(yh, 2), hr2 = readlane(yh, 3);
+    const double yl2 = (wid == 0) ? hl2 : el2, yl1 = (wid == 0) ? hl1 : el1;
+    const double yr1 = (wid == W - 1) ? hr1 : er1, yr2 = (wid == W - 1) ? hr2 : er2;
+    // lane l-1 / l+1 hold columns 2l-2, 2l-1 / 2l+2, 2l+3 (whole-wave DPP shifts)
+    const double ux = dpp_up(u.x), uy = dpp_up(u.y);
+    const double dx = dpp_down(u.x), dy = dpp_down(u.y);
+    const double cm2 = (lane == 0) ? yl2 : ux, cm1 = (lane == 0) ? yl1 : uy;
+    const double cp2 = (lane == 63) ? yr1 : dx, cp3 = (lane == 63) ? yr2 : dy;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      yw[m] = yw[m + 1];
+      hw[m] = hw[m + 1];
+      vw[m] = vw[m + 1];
+    }
+    yw[4] = u;
+    hw[4] = dv2{cm1 + u.y, u.x + cp2};
+    vw[4] = v;
+    const bool st = own && q >= r0 && q < r1;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
+                                           st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
+    if (A.Eout_v)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
+                                             st ? eoff(q) : kOOB, 0, 0);
+    return dv2{cm2 + cp2, cm1 + cp3};
+  };
+
+  double aw[NV + 3], ag[NV];  // aw: w'.V_i, then w'.v, v.v, w'.w'
+#pragma unroll
+  for (int i = 0; i < NV + 3; ++i) aw[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) ag[i] = 0.0;
+  dv2 h2w[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
+  const double zs = A.alpha * isc;
+  auto centre = [&](int64_t r) {  // closed-form FD quotient as in arnoldi_kernel
+    const dv2 (*d)[64] = lg[(r - r0) & 1];
+    const dv2 x0r = d[NV][lane];
+    dv2 wo;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double uc = yw[2][q];
+      const double a1 = hw[2][q] + (yw[1][q] + yw[3][q]);
+      const double dg = hw[1][q] + hw[3][q];
+      const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
+      const double Lu = applyL13(K, uc, a1, dg, a2);
+      const double x = x0r[q];
+      const double t = A.alpha * uc;
+      const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
+      wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
+    }
+    const bool in = own && r < r1;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
+                                           in ? uint32_t((r * nx + col) * 8) : kOOB, 0, 0);
+    if (A.Eout_w)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
+                                             in ? eoff(r) : kOOB, 0, 0);
+    const dv2 wm = in ? wo : dv2{0.0, 0.0};
+    const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const dv2 bi = d[i][lane];
+      aw[i] = __builtin_fma(wm.y, bi.y, __builtin_fma(wm.x, bi.x, aw[i]));
+      ag[i] = __builtin_fma(vm.y, bi.y, __builtin_fma(vm.x, bi.x, ag[i]));
+    }
+    aw[NV] = __builtin_fma(wm.y, vm.y, __builtin_fma(wm.x, vm.x, aw[NV]));
+    aw[NV + 1] = __builtin_fma(vm.y, vm.y, __builtin_fma(vm.x, vm.x, aw[NV + 1]));
+    aw[NV + 2] = __builtin_fma(wm.y, wm.y, __builtin_fma(wm.x, wm.x, aw[NV + 2]));
+  };
+  auto push_h2 = [&](const Slot& s, int64_t q) {
+    const dv2 h2 = push(s, q);
+    h2w[0] = h2w[1];
+    h2w[1] = h2w[2];
+    h2w[2] = h2;
+  };
+
+  if (nrows > 0) {
+    Slot P[2];
+    load(P[0], r0 - 2);
+    load(P[1], r0 - 1);
+    push_h2(P[0], r0 - 2);
+    push_h2(P[1], r0 - 1);
+    load(P[0], r0);
+    load(P[1], r0 + 1);
+    Slot S[RR];
+#pragma unroll
+    for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
+    push_h2(P[0], r0);
+    stash(P[0], gq, r0);
+    push_h2(P[1], r0 + 1);
+    stash(P[1], gq, r0 + 1);
+    for (int64_t t0 = 0; t0 < nrows; t0 += RR) {  // no branch inside a group (see arnoldi_kernel)
+#pragma unroll
+      for (int k = 0; k < RR; ++k) {
+        const int64_t r = r0 + t0 + k;
+        load(S[(k + PF) % RR], r + 2 + PF);
+        push_h2(S[k], r + 2);
+        centre(r);
+        stash(S[k], gq, r + 2);
+      }
+    }
+  }
+
+  wave_sum<NV + 3>(aw);
+  wave_sum<NV>(ag);
+  if (lane == 0) {
+    const int64_t nw = A.pstride;
+    double* p = A.partial + A.pcol0 + gw;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      p[int64_t(i) * nw] = aw[i];
+      p[int64_t(NV + 1 + i) * nw] = ag[i];
+    }
+    p[int64_t(NV) * nw] = aw[NV];
+    p[int64_t(2 * NV + 1) * nw] = aw[NV + 1];
+    p[int64_t(2 * NV + 2) * nw] = aw[NV + 2];
+  }
+}
+
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return (v && *v) ? std::atoi(v) : dflt;
@@ -566,34 +863,21 @@ struct Occ {
   int ncu = 0, blocks_per_cu = 0;
 };
 
-template <int NV, bool EXT, int PF, bool NT>
-hipError_t launch_t(ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
-  auto kern = arnoldi_kernel<NV, EXT, PF, NT>;
-  if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
-  // per instantiation, filled once by a thread-safe static initialiser (slab threads of the
-  // loopback communicator launch the same instantiation concurrently)
-  static const Occ occ = [&] {
-    Occ o;
-    int dev = 0, ncu = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 64 * WPB, 0) != hipSuccess)
-      return o;  // ncu == 0: reported below
-    o.blocks_per_cu = nb > 0 ? nb : 1;
-    o.ncu = ncu > 0 ? ncu : 1;
-    return o;
-  }();
+// Grid of one resident round of waves (NKHIP_ARN_ROUNDS scales it) for a kernel whose blocks own
+// `nwb` waves of `cw` columns each; bands of >= 8 rows, and no more partial columns than the
+// caller's buffer holds.  `occ` = that kernel's occupancy.
+template <int NV, class K>
+hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, hipStream_t s,
+                       int64_t* nwaves) {
   if (occ.ncu == 0) return hipErrorUnknown;
-  // one resident round of waves (NKHIP_ARN_ROUNDS scales it); bands of >= 8 rows, and no more
-  // partial columns than the caller's buffer holds
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
-  const int64_t strips = (A.nx + kSW - 1) / kSW;
+  const int64_t strips = (A.nx + cw - 1) / cw;
   const int64_t rb = A.r_begin, re = (A.r_end >= 0) ? A.r_end : A.ny;
   if (rb < 0 || re > A.ny || re <= rb) return hipErrorInvalidValue;
   const int64_t rows = re - rb;
   const int64_t ncu_use = (occ.ncu - A.reserve_cus > 0) ? occ.ncu - A.reserve_cus : 1;
-  const int64_t target = ncu_use * occ.blocks_per_cu * WPB * (rounds > 0 ? rounds : 1);
-  const int64_t wpr = (strips + WPB - 1) / WPB * WPB;  // waves per band (whole blocks)
+  const int64_t target = ncu_use * occ.blocks_per_cu * nwb * (rounds > 0 ? rounds : 1);
+  const int64_t wpr = (strips + nwb - 1) / nwb * nwb;  // waves per band (whole blocks)
   int64_t nbands = target / wpr;
   const int64_t cap_bands = A.partial_cap / ((2 * int64_t(NV) + 3) * wpr);
   if (nbands > cap_bands) nbands = cap_bands;
@@ -613,11 +897,42 @@ hipError_t launch_t(ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
   A.strips = int(strips);
   A.nbands = int(nbands);
   A.RY = int(RY);
-  int64_t blocks = (nw + WPB - 1) / WPB;
+  int64_t blocks = (nw + nwb - 1) / nwb;
   blocks = (blocks + 7) / 8 * 8;
   *nwaves = nw;
-  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * WPB), 0, s, A);
+  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * nwb), 0, s, A);
   return hipGetLastError();
+}
+
+// occupancy of one kernel instantiation, queried once by a thread-safe static initialiser (slab
+// threads of the loopback communicator launch the same instantiation concurrently)
+template <class K>
+Occ query_occ(K kern, int threads) {
+  Occ o;
+  int dev = 0, ncu = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess)
+    return o;  // ncu == 0: reported by launch_grid
+  o.blocks_per_cu = nb > 0 ? nb : 1;
+  o.ncu = ncu > 0 ? ncu : 1;
+  return o;
+}
+
+template <int NV, bool EXT, int PF, bool NT>
+hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
+  auto kern = arnoldi_kernel<NV, EXT, PF, NT>;
+  if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
+  static const Occ occ = query_occ(kern, 64 * WPB);
+  return launch_grid<NV>(kern, occ, WPB, kSW, A, s, nwaves);
+}
+
+constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
+template <int NV, bool EXT, int PF, bool NT>
+hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
+  auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW>;
+  static const Occ occ = query_occ(kern, 64 * kWideW);
+  return launch_grid<NV>(kern, occ, kWideW, kWW, A, s, nwaves);
 }
 
 template <int NV, bool EXT>
@@ -637,6 +952,13 @@ hipError_t launch_pf(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
     }
   }
 #endif
+  if constexpr (NV <= kWideMaxNV) {
+    if (arnoldi_wide(NV)) {
+      constexpr int PFW = NV <= 4 ? 3 : (NV <= 10 ? 2 : 1);
+      return nt ? launch_wide<NV, EXT, PFW, true>(A, s, nwaves)
+                : launch_wide<NV, EXT, PFW, false>(A, s, nwaves);
+    }
+  }
   return nt ? launch_t<NV, EXT, PF, true>(A, s, nwaves) : launch_t<NV, EXT, PF, false>(A, s, nwaves);
 }
 
@@ -659,9 +981,11 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
 }
 
 // u (= v, or z) on the edge rows 0, 1, ny-2, ny-1 of a slab (grid: column blocks x 4 rows).
-// The update sum runs in the fused kernel's order -- entries 0, 2, 4, .. of [V_0 .. V_{nv-1}, w] in one partial,
-// 1, 3, 5, .. in the other, then their sum -- so a halo row equals the row its owner computes.
-__global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4) {
+// The update sum runs in the fused kernel's order -- for the pair layout entries 0, 2, 4, .. of
+// [V_0 .. V_{nv-1}, w] in one partial, 1, 3, 5, .. in the other, then their sum; for the wide
+// layout (seq) one sum in entry order -- so a halo row equals the row its owner computes.
+__global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4,
+                                                           bool seq) {
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (j >= A.nx) return;
   const int t = blockIdx.y;
@@ -678,6 +1002,16 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
     auto cof = [&](int e) -> double { return (e < A.nv) ? A.c[e] : A.tau; };
     double p0 = 0.0, p1 = 0.0;
     int e = 0;
+    if (seq) {  // the wide layout's order: one sum over the entries in order
+      for (; e + 8 <= ne; e += 8) {
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = ent(e + q)[o];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p0 += cof(e + q) * x[q];
+      }
+      for (; e < ne; ++e) p0 += cof(e) * ent(e)[o];
+    }
     for (; e + 8 <= ne; e += 8) {
       double x[8];
 #pragma unroll
@@ -729,8 +1063,13 @@ hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) {
   if (A.ny < 4 || A.nx < 1 || !y4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(arnoldi_edge_kernel, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256), 0, s,
-                     A, y4);
+                     A, y4, A.nv <= kWideMaxNV && arnoldi_wide(A.nv));
   return hipGetLastError();
+}
+
+bool arnoldi_wide(int nv) {
+  static const bool on = env_int("NKHIP_ARN_WIDE", 1) != 0;
+  return on && nv <= kWideMaxNV;
 }
 
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx) {

@@ -127,8 +127,8 @@ constexpr int kArnMaxNV = 35;
 // consecutive rows share a line.  The fused kernel writes the edge arrays of its two outputs;
 // other producers of update entries run edge_gather_launch.
 constexpr int kEdgeW = 256;
-inline int64_t edge_groups(int64_t nx) { return (nx + kEdgeW - 1) / kEdgeW; }
-inline int64_t edge_elems(int64_t ny, int64_t nx) { return edge_groups(nx) * ny * 4; }
+__host__ __device__ inline int64_t edge_groups(int64_t nx) { return (nx + kEdgeW - 1) / kEdgeW; }
+__host__ __device__ inline int64_t edge_elems(int64_t ny, int64_t nx) { return edge_groups(nx) * ny * 4; }
 hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx, hipStream_t s);
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;
@@ -166,6 +166,8 @@ struct ArnoldiArgs {
                                    // halo exchange needs CUs for its kernels)
 };
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
+// basis length nv runs the wide layout (128-column waves, 512-column blocks; NKHIP_ARN_WIDE=0: off)
+bool arnoldi_wide(int nv);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
 // u = v (or z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
