@@ -168,6 +168,8 @@ struct ArnoldiArgs {
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // basis length nv runs the wide layout (128-column waves, 512-column blocks; NKHIP_ARN_WIDE=0: off)
 bool arnoldi_wide(int nv);
+// basis length nv runs the split layout (128-column waves, entry halves on two waves; NKHIP_ARN_SPLIT=0: off)
+bool arnoldi_split(int nv);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
 // u = v (or z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
