@@ -65,6 +65,7 @@ typedef struct nk_stats {
   int64_t n_backtrack; /* Newton iterations whose Armijo step s was < 1 (scalar_search_armijo,
                           scipy/optimize/_linesearch.py:684-739) */
   double step_min;     /* smallest accepted line-search step (1 when none backtracked) */
+  int64_t n_device_steps; /* Arnoldi steps whose control ran on the device (arnctl.hip) */
 } nk_stats;
 
 /* Per-kernel-class timings recorded with HIP events on the solver's stream. */

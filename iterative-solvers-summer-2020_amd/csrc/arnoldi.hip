@@ -91,6 +91,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(double* p, int64_t n) {
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(uint32_t(n * 8)), 0x00020000);
 }
 
+// Per-step scalars of a fused launch: the kernel arguments, or -- under device-side Arnoldi
+// control -- the parameter block the control kernel wrote (nk_kernels.h kCtlPrm).  Read once,
+// before a kernel's row loop (a load inside it would join the row's wait-count queue).  The
+// block is read through a buffer resource (no records when there is none), so both sources are
+// plain loads and the selection never turns into one load through a merged generic pointer.
+__device__ __forceinline__ double arn_prm(const ArnoldiArgs& A, int i, double arg) {
+  const __amdgpu_buffer_rsrc_t r = rsrc(const_cast<double*>(A.ctl), A.ctl ? kCtlPrm : 0);
+  const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, uint32_t(i) * 8, 0, 0));
+  return A.ctl ? v : arg;
+}
+__device__ __forceinline__ double arn_c(const ArnoldiArgs& A, int e) { return arn_prm(A, e, A.c[e]); }
+__device__ __forceinline__ double arn_tau(const ArnoldiArgs& A) { return arn_prm(A, kArnMaxNV, A.tau); }
+__device__ __forceinline__ double arn_alpha(const ArnoldiArgs& A) {
+  return arn_prm(A, kArnMaxNV + 1, A.alpha);
+}
+__device__ __forceinline__ double arn_sc(const ArnoldiArgs& A) { return arn_prm(A, kArnMaxNV + 2, A.sc); }
+// the control kernel handed the loop back to the host: the queued launch does nothing (read in
+// the same batch as the parameters: one load latency at kernel start)
+__device__ __forceinline__ bool arn_halted(const ArnoldiArgs& A) {
+  return arn_prm(A, kArnMaxNV + 3, 0.0) != 0.0;
+}
+
 // Rows of loads in flight per wave for a basis of NV vectors (register budget at one or two
 // waves per SIMD; the wait counter tracks at most 63 loads)
 constexpr int pf_for(int nv) { return nv <= 4 ? 3 : nv <= 20 ? 2 : 1; }
@@ -187,6 +209,11 @@ __device__ __forceinline__ double dpp_down(double x) {
 // entries (half 0 also w'.v, v.v, w'.w').
 template <int NV, bool EXT, int PF, bool NT>
 __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) {
+  const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
+  double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
+#pragma unroll
+  for (int e = 0; e < NV; ++e) cst[e] = arn_c(A, e);
+  if (arn_halted(A)) return;
   constexpr int RR = PF + 1;               // register ring: the update row and PF rows in flight
   constexpr int NE = NV + 2 + (EXT ? 1 : 0);
   constexpr int NI = (NE + 1) / 2;         // 16-B loads per row and lane
@@ -224,7 +251,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
   const int64_t nrows = r1 - r0;
   const SHCoef& K = A.k;
-  const double isc = 1.0 / A.sc;
+  const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
   dv2 (*lg)[NB + 1][64] = lag[wid];
@@ -241,7 +268,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       if (e == EX) return A.x0;
       return EXT ? A.z : A.x0;
     };
-    auto cof = [&](int e) -> double { return e < NV ? A.c[e] : (e == NV ? A.tau : 0.0); };
+    auto cof = [&](int e) -> double { return e < NV ? cst[e] : (e == NV ? a_tau : 0.0); };
     const int e0 = 2 * k, e1 = (2 * k + 1 < NE) ? 2 * k + 1 : 2 * k;
     ep[k] = hf ? src(e1) : src(e0);
     ecf[k] = hf ? (2 * k + 1 < NE ? cof(e1) : 0.0) : cof(e0);
@@ -258,10 +285,10 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       p = (e == j) ? A.V[j] : p;
-      cf = (e == j) ? A.c[j] : cf;
+      cf = (e == j) ? cst[j] : cf;
     }
     p = (e == NV) ? A.w : p;
-    cf = (e == NV) ? A.tau : cf;
+    cf = (e == NV) ? a_tau : cf;
     hp = p;
     hcf = cf;
   }
@@ -467,7 +494,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   // stencil, so the difference quotient is exactly
   //   (a/sc) [u/k - (L u + u (g (2 x0 + t) - (3 x0 (x0 + t) + t^2)))/2],  t = a u,
   // without the cancellation of two G evaluations (and without reading G0).
-  const double zs = A.alpha * isc;
+  const double zs = a_alpha * isc;
   auto centre = [&](int64_t r) {
     const dv2 (*d)[64] = lg[(r - r0) & 1];
     const dv2 x0r = d[NB][lane];
@@ -480,7 +507,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
       const double Lu = applyL13(K, uc, a1, dg, a2);
       const double x = x0r[q];
-      const double t = A.alpha * uc;
+      const double t = a_alpha * uc;
       const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
       wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
     }
@@ -589,10 +616,14 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 // bases.  The update sum runs over the entries in order (arnoldi_edge_kernel matches it).
 constexpr int kWW = 128;       // columns per wave
 constexpr int kWideMaxNV = 18;  // LDS: 2 rows x (nv + 1) x 4 waves x 1 KB <= 152 KB
-constexpr int kSplitMaxNV = 30;  // arnoldi_split_kernel: above this its registers spill
 
 template <int NV, bool EXT, int PF, bool NT, int W>
 __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs A) {
+  const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
+  double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
+#pragma unroll
+  for (int e = 0; e < NV; ++e) cst[e] = arn_c(A, e);
+  if (arn_halted(A)) return;
   constexpr int RR = PF + 1;
   constexpr int NE = NV + 2 + (EXT ? 1 : 0);  // [V_0 .. V_{NV-1}, w, x0, (z)]
   constexpr int EX = NV + 1, EZ = NV + 2;
@@ -622,7 +653,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
   const int64_t nrows = r1 - r0;
   const SHCoef& K = A.k;
-  const double isc = 1.0 / A.sc;
+  const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
   dv2 (*lg)[NV + 1][64] = lag[wid];
@@ -632,7 +663,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     if (e == EX) return A.x0;
     return A.z;
   };
-  auto cof = [&](int e) -> double { return e < NV ? A.c[e] : A.tau; };  // e <= NV
+  auto cof = [&](int e) -> double { return e < NV ? cst[e] : a_tau; };  // e <= NV
   // packed block-halo loads: lane 4e' + hh of wave w fetches column hh of entry w + W e'
   const double *hp, *hE;
   double hcf;
@@ -645,9 +676,9 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     for (int j = 0; j < NV; ++j) {
       p = (e == j) ? A.V[j] : p;
       pe = (e == j) ? A.E[j] : pe;
-      cf = (e == j) ? A.c[j] : cf;
+      cf = (e == j) ? cst[j] : cf;
     }
-    cf = (e == NV) ? A.tau : cf;
+    cf = (e == NV) ? a_tau : cf;
     hp = p;
     hE = pe;
     hcf = cf;
@@ -787,7 +818,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   dv2 h2w[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
-  const double zs = A.alpha * isc;
+  const double zs = a_alpha * isc;
   auto centre = [&](int64_t r) {  // closed-form FD quotient as in arnoldi_kernel
     const dv2 (*d)[64] = lg[(r - r0) & 1];
     const dv2 x0r = d[NV][lane];
@@ -800,7 +831,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
       const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
       const double Lu = applyL13(K, uc, a1, dg, a2);
       const double x = x0r[q];
-      const double t = A.alpha * uc;
+      const double t = a_alpha * uc;
       const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
       wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
     }
@@ -872,344 +903,6 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Split layout (basis lengths above kWideMaxNV): 128-column waves and 1-KB row segments as in the
-// wide layout, but a block's four waves are two column groups (256 columns) x two halves of the
-// update entries: half 0 streams V_0 .. V_{H0-1}, half 1 V_{H0} .. V_{NV-1}, w, x0 (and z), so a
-// lane holds about half the entries of the wide layout (registers) and the LDS lag holds each
-// basis row once (2 rows x (nv+1) x 256 columns, as the pair layout).  The two halves exchange
-// their partial update sums through LDS after the row's barrier; both then hold v (summed as
-// half 0 + half 1, in entry order inside each half: arnoldi_edge_kernel matches it), both form
-// the stencil, each takes the dot products of its own entries.
-template <int NV, bool EXT, int PF, bool NT>
-__global__ void __launch_bounds__(256) arnoldi_split_kernel(const ArnoldiArgs A) {
-  constexpr int RR = PF + 1;
-  constexpr int H0 = (NV + 2 + (EXT ? 1 : 0) + 1) / 2;  // half 0's loads (basis entries only)
-  static_assert(H0 <= NV, "half 1 holds w");
-  constexpr int NB1 = NV - H0;                 // basis entries of half 1
-  constexpr int N1 = NB1 + 2 + (EXT ? 1 : 0);  // half 1's loads: its basis entries, w, x0, (z)
-  constexpr int NS = H0 > N1 ? H0 : N1;        // loads per row and lane (the larger half)
-  constexpr int LS = H0;                       // lag slots a wave writes (half 1: NB1 < H0 used)
-  static_assert(NV + 1 <= 64, "one packed halo load per row");
-  // LDS (163.2 KB of 160 KiB at nv = 35): basis rows r, r+1 of both halves (half 0 in slots
-  // [0, H0), half 1 in [H0, NV)); x0 of rows r..r+2 (half 1); the partial sums; u where it is not
-  // v (half 1); a scratch row for the stores a wave makes only to keep its code branch-free
-  __shared__ dv2 lag[2][2][NV][64];
-  __shared__ dv2 xlag[3][2][64];
-  __shared__ dv2 xch[2][2][2][64];
-  __shared__ dv2 ualt[2][2][64];
-  __shared__ dv2 dummy[64];
-  __shared__ double hpart[2][4][4];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int cg = wid >> 1, eh = wid & 1;
-  const int64_t b = blockIdx.x;
-  const int64_t bpx = gridDim.x / 8;
-  const int64_t L = (b % 8) * bpx + b / 8;
-  const int64_t ngroups = (A.strips + 1) / 2;
-  if (L >= ngroups * A.nbands) return;
-  const int64_t band = L / ngroups, grp = L % ngroups;
-  const int64_t gw = L * 2 + cg;  // partial column of this column group (both halves write it)
-  const int64_t nx = A.nx, ny = A.ny;
-  const int64_t B0 = grp * 2 * kWW;
-  const int64_t c = B0 + cg * kWW + 2 * lane;
-  const int64_t col = c % nx;
-  const bool own = c < nx;
-  const int hh = lane & 3;
-  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + 2 * kWW - 2 + hh;
-  const int64_t hcol = ((hc % nx) + nx) % nx;
-  const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
-  const int64_t r0 = A.r_begin + band * A.RY;
-  const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
-  const int64_t nrows = r1 - r0;
-  const SHCoef& K = A.k;
-  const double isc = 1.0 / A.sc;
-  const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
-  const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
-  const int lb = eh ? H0 : 0;  // this half's first lag slot
-  // load k of this wave: entry index (wave-uniform); the smaller half's surplus loads repeat its
-  // first entry (an L1 hit) with coefficient 0
-  constexpr int EX = NV + 1, EZ = NV + 2;
-  auto ent = [&](int k) -> int {
-    if (eh == 0) return k < H0 ? k : 0;
-    if (k < NB1) return H0 + k;
-    if (k == NB1) return NV;  // w
-    if (k == NB1 + 1) return EX;
-    return (EXT && k == NB1 + 2) ? EZ : H0;
-  };
-  auto src = [&](int e) -> const double* {
-    if (e < NV) return A.V[e];
-    if (e == NV) return A.w;
-    if (e == EX) return A.x0;
-    return A.z;
-  };
-  const int nupd = eh ? NB1 + 1 : H0;  // update entries of this half (w included in half 1)
-  const double* ep[NS];
-  double ecf[NS];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    const int e = ent(k);
-    ep[k] = src(e);
-    ecf[k] = (k < nupd) ? (e < NV ? A.c[e] : A.tau) : 0.0;
-  }
-  const double *hp, *hE;  // packed block-halo loads over the four waves
-  double hcf;
-  {
-    const int e = wid + 4 * (lane >> 2);
-    const double* p = A.w;
-    const double* pe = A.E[NV];
-    double cf = 0.0;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      p = (e == j) ? A.V[j] : p;
-      pe = (e == j) ? A.E[j] : pe;
-      cf = (e == j) ? A.c[j] : cf;
-    }
-    cf = (e == NV) ? A.tau : cf;
-    hp = p;
-    hE = pe;
-    hcf = cf;
-  }
-  const bool useE = A.E[0] != nullptr;
-  const int64_t nbE = edge_groups(nx);
-  const int64_t bL = B0 / kEdgeW, bR = ((B0 + 2 * kWW) / kEdgeW) % nbE;
-  const bool eL = own && (c % kEdgeW == 0);
-  const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
-  const int64_t ebo =
-      eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
-  const bool eOn = eL || eR;
-  const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
-  auto eoff = [&](int64_t q) -> uint32_t {
-    return eOn ? uint32_t(((ebo / 4) * ny * 4 + q * 4 + (ebo & 3)) * 8) : kOOB;
-  };
-  const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;
-  const bool slab = A.yh != nullptr;
-  const double* yhb = slab ? A.yh : A.x0;
-  auto wrap = [&](int64_t q) -> int64_t {
-    q = (q > r1 + 1) ? r1 + 1 : q;
-    return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
-  };
-
-  struct Slot {
-    dv2 e[NS];
-    double hv, hx;
-    bool own;
-  };
-  auto load = [&](Slot& s, int64_t q) {
-    const int64_t qq = wrap(q);
-    const int64_t o = qq * nx + col;
-    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
-    const bool hrow = slab && (qc < 0 || qc >= ny);
-    const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      const double* a = ep[k] + o;
-      if (k == NB1 + 1) a = (hrow && eh == 1) ? yhb + hq * nx + col : a;  // half 1's x0 entry
-      s.e[k] = gld2<NT>(a);
-    }
-    const int64_t ho = qq * nx + hcol;
-    const int64_t eo = ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh;
-    if constexpr (!EXT) s.hv = gld(useE ? hE + eo : hp + ho);
-    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
-    s.own = !hrow;
-  };
-  // own basis rows (and, for half 1, x0 into the 3-row x0 ring) until row q's dot products;
-  // stores past a half's own entries go to the scratch row (no branch)
-  auto stash = [&](const Slot& s, int64_t q) {
-    dv2 (*d)[64] = lag[(q - r0) & 1][cg];
-#pragma unroll
-    for (int k = 0; k < LS; ++k) {
-      dv2* dst = (eh && k >= NB1) ? dummy : d[lb + k];
-      dst[lane] = s.e[k];
-    }
-    (eh ? xlag[int((q - r0 + 3) % 3)][cg] : dummy)[lane] = s.e[NB1 + 1];
-  };
-
-  dv2 yw[5], hw[5], vw[5];
-#pragma unroll
-  for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
-  auto push = [&](const Slot& s, int64_t q) {
-    dv2 p{0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      p.x += ecf[k] * s.e[k].x;
-      p.y += ecf[k] * s.e[k].y;
-    }
-    const int slot = int(q & 1);
-    xch[slot][cg][eh][lane] = p;
-    {
-      const dv2 xe = s.e[NB1 + 1];
-      dv2 ua = xe;
-      if constexpr (EXT) ua = s.own ? s.e[NB1 + 2] : xe;
-      (eh ? ualt[slot][cg] : dummy)[lane] = ua;  // half 1's x0 / z entries
-    }
-    if constexpr (!EXT) {
-      double hs = hcf * s.hv;
-      hs += dpp_row_shr(hs, 4);
-      hs += dpp_row_shr(hs, 8);
-      hs = pair16_sum(hs);
-      hs = pair_sum(hs);
-      if ((lane & ~3) == 12) hpart[slot][wid][lane & 3] = hs;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    const dv2 p0 = xch[slot][cg][0][lane], p1 = xch[slot][cg][1][lane];
-    const dv2 v{p0.x + p1.x, p0.y + p1.y};
-    const dv2 ua = ualt[slot][cg][lane];
-    dv2 u;
-    if constexpr (EXT)
-      u = ua;
-    else
-      u = s.own ? v : ua;
-    double hz = 0.0;
-    if constexpr (EXT) {
-      hz = __shfl(s.hx, hh + 4, 64);
-    } else {
-#pragma unroll
-      for (int w = 0; w < 4; ++w) hz += hpart[slot][w][hh];
-    }
-    const double yh = s.own ? hz : s.hx;
-    // the other column group's edge columns: from its u, recomputed here from the exchanged
-    // partial sums (no second barrier)
-    const int oc = cg ^ 1;
-    const dv2 q0 = xch[slot][oc][0][cg ? 63 : 0], q1 = xch[slot][oc][1][cg ? 63 : 0];
-    const dv2 ov{q0.x + q1.x, q0.y + q1.y};
-    const dv2 oa = ualt[slot][oc][cg ? 63 : 0];
-    dv2 ou;
-    if constexpr (EXT)
-      ou = oa;
-    else
-      ou = s.own ? ov : oa;
-    const double hl2 = readlane(yh, 0), hl1 = readlane(yh, 1);
-    const double hr1 = readlane(yh, 2), hr2 = readlane(yh, 3);
-    // column group 0: left = block halo, right = group 1's columns 0, 1; group 1: left = group
-    // 0's columns 126, 127, right = block halo
-    const double yl2 = cg ? ou.x : hl2, yl1 = cg ? ou.y : hl1;
-    const double yr1 = cg ? hr1 : ou.x, yr2 = cg ? hr2 : ou.y;
-    const double ux = dpp_up(u.x), uy = dpp_up(u.y);
-    const double dx = dpp_down(u.x), dy = dpp_down(u.y);
-    const double cm2 = (lane == 0) ? yl2 : ux, cm1 = (lane == 0) ? yl1 : uy;
-    const double cp2 = (lane == 63) ? yr1 : dx, cp3 = (lane == 63) ? yr2 : dy;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      yw[m] = yw[m + 1];
-      hw[m] = hw[m + 1];
-      vw[m] = vw[m + 1];
-    }
-    yw[4] = u;
-    hw[4] = dv2{cm1 + u.y, u.x + cp2};
-    vw[4] = v;
-    const bool st = own && eh == 0 && q >= r0 && q < r1;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
-                                           st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
-    if (A.Eout_v)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
-                                             st ? eoff(q) : kOOB, 0, 0);
-    return dv2{cm2 + cp2, cm1 + cp3};
-  };
-
-  double aw[LS], ag[LS], a3[3] = {0.0, 0.0, 0.0};  // own w'.V_i, v.V_i; w'.v, v.v, w'.w'
-#pragma unroll
-  for (int i = 0; i < LS; ++i) aw[i] = ag[i] = 0.0;
-  dv2 h2w[3];
-#pragma unroll
-  for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
-  const double zs = A.alpha * isc;
-  auto centre = [&](int64_t r) {
-    const dv2 (*d)[64] = lag[(r - r0) & 1][cg];
-    const dv2 x0r = xlag[int((r - r0 + 3) % 3)][cg][lane];
-    dv2 wo;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const double uc = yw[2][q];
-      const double a1 = hw[2][q] + (yw[1][q] + yw[3][q]);
-      const double dg = hw[1][q] + hw[3][q];
-      const double a2 = h2w[0][q] + (yw[0][q] + yw[4][q]);
-      const double Lu = applyL13(K, uc, a1, dg, a2);
-      const double x = x0r[q];
-      const double t = A.alpha * uc;
-      const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
-      wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
-    }
-    const bool in = own && r < r1;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           (in && eh == 1) ? uint32_t((r * nx + col) * 8) : kOOB,
-                                           0, 0);
-    if (A.Eout_w)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
-                                             (in && eh == 1) ? eoff(r) : kOOB, 0, 0);
-    const dv2 wm = in ? wo : dv2{0.0, 0.0};
-    const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < LS; ++i) {
-      // (half 1 past its NB1 entries: a valid slot, the sums are never written out)
-      const dv2 bi = d[(lb + i < NV) ? lb + i : NV - 1][lane];
-      aw[i] = __builtin_fma(wm.y, bi.y, __builtin_fma(wm.x, bi.x, aw[i]));
-      ag[i] = __builtin_fma(vm.y, bi.y, __builtin_fma(vm.x, bi.x, ag[i]));
-    }
-    const dv2 wh = eh ? dv2{0.0, 0.0} : wm, vh = eh ? dv2{0.0, 0.0} : vm;  // half 0 only
-    a3[0] = __builtin_fma(wh.y, vm.y, __builtin_fma(wh.x, vm.x, a3[0]));
-    a3[1] = __builtin_fma(vh.y, vm.y, __builtin_fma(vh.x, vm.x, a3[1]));
-    a3[2] = __builtin_fma(wh.y, wm.y, __builtin_fma(wh.x, wm.x, a3[2]));
-  };
-  auto push_h2 = [&](const Slot& s, int64_t q) {
-    const dv2 h2 = push(s, q);
-    h2w[0] = h2w[1];
-    h2w[1] = h2w[2];
-    h2w[2] = h2;
-  };
-
-  if (nrows > 0) {
-    Slot P[2];
-    load(P[0], r0 - 2);
-    load(P[1], r0 - 1);
-    push_h2(P[0], r0 - 2);
-    push_h2(P[1], r0 - 1);
-    load(P[0], r0);
-    load(P[1], r0 + 1);
-    Slot S[RR];
-#pragma unroll
-    for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
-    push_h2(P[0], r0);
-    stash(P[0], r0);
-    push_h2(P[1], r0 + 1);
-    stash(P[1], r0 + 1);
-    for (int64_t t0 = 0; t0 < nrows; t0 += RR) {
-#pragma unroll
-      for (int k = 0; k < RR; ++k) {
-        const int64_t r = r0 + t0 + k;
-        load(S[(k + PF) % RR], r + 2 + PF);
-        push_h2(S[k], r + 2);
-        centre(r);
-        stash(S[k], r + 2);
-      }
-    }
-  }
-
-  wave_sum<LS>(aw);
-  wave_sum<LS>(ag);
-  wave_sum<3>(a3);
-  if (lane == 0) {
-    const int64_t nw = A.pstride;
-    double* p = A.partial + A.pcol0 + gw;
-    const int i0 = eh ? H0 : 0, ni = eh ? NB1 : H0;
-#pragma unroll
-    for (int k = 0; k < LS; ++k) {
-      if (k < ni) {
-        p[int64_t(i0 + k) * nw] = aw[k];
-        p[int64_t(NV + 1 + i0 + k) * nw] = ag[k];
-      }
-    }
-    if (eh == 0) {
-      p[int64_t(NV) * nw] = a3[0];
-      p[int64_t(2 * NV + 1) * nw] = a3[1];
-      p[int64_t(2 * NV + 2) * nw] = a3[2];
-    }
-  }
-}
-
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return (v && *v) ? std::atoi(v) : dflt;
@@ -1224,7 +917,7 @@ struct Occ {
 // caller's buffer holds.  `occ` = that kernel's occupancy.
 template <int NV, class K>
 hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, hipStream_t s,
-                       int64_t* nwaves, int threads = 0) {
+                       int64_t* nwaves) {
   if (occ.ncu == 0) return hipErrorUnknown;
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
   const int64_t strips = (A.nx + cw - 1) / cw;
@@ -1256,7 +949,7 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, h
   int64_t blocks = (nw + nwb - 1) / nwb;
   blocks = (blocks + 7) / 8 * 8;
   *nwaves = nw;
-  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(threads ? threads : 64 * nwb), 0, s, A);
+  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * nwb), 0, s, A);
   return hipGetLastError();
 }
 
@@ -1281,13 +974,6 @@ hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
   static const Occ occ = query_occ(kern, 64 * WPB);
   return launch_grid<NV>(kern, occ, WPB, kSW, A, s, nwaves);
-}
-
-template <int NV, bool EXT, int PF, bool NT>
-hipError_t launch_split(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
-  auto kern = arnoldi_split_kernel<NV, EXT, PF, NT>;
-  static const Occ occ = query_occ(kern, 256);
-  return launch_grid<NV>(kern, occ, 2, kWW, A, s, nwaves, 256);
 }
 
 constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
@@ -1322,13 +1008,6 @@ hipError_t launch_pf(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
                 : launch_wide<NV, EXT, PFW, false>(A, s, nwaves);
     }
   }
-  if constexpr (NV > kWideMaxNV && NV <= kSplitMaxNV) {
-    if (arnoldi_split(NV)) {
-      constexpr int PFS = 1;
-      return nt ? launch_split<NV, EXT, PFS, true>(A, s, nwaves)
-                : launch_split<NV, EXT, PFS, false>(A, s, nwaves);
-    }
-  }
   return nt ? launch_t<NV, EXT, PF, true>(A, s, nwaves) : launch_t<NV, EXT, PF, false>(A, s, nwaves);
 }
 
@@ -1353,10 +1032,12 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
 // u (= v, or z) on the edge rows 0, 1, ny-2, ny-1 of a slab (grid: column blocks x 4 rows).
 // The update sum runs in the fused kernel's order -- for the pair layout (h0 = 0) entries 0, 2,
 // 4, .. of [V_0 .. V_{nv-1}, w] in one partial, 1, 3, 5, .. in the other, then their sum; for the
-// wide and split layouts entries [0, h0) and [h0, nv] in order, then their sum -- so a halo row
+// wide layout (h0 = nv + 1) all entries in order -- so a halo row
 // equals the row its owner computes.
 __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4,
                                                            int h0) {
+  const double a_tau = arn_tau(A);
+  if (arn_halted(A)) return;
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (j >= A.nx) return;
   const int t = blockIdx.y;
@@ -1370,10 +1051,10 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
     // 4 rows of a slab); the sums stay in entry order within each parity
     const int ne = A.nv + 1;
     auto ent = [&](int e) -> const double* { return (e < A.nv) ? A.V[e] : A.w; };
-    auto cof = [&](int e) -> double { return (e < A.nv) ? A.c[e] : A.tau; };
+    auto cof = [&](int e) -> double { return (e < A.nv) ? arn_c(A, e) : a_tau; };
     double p0 = 0.0, p1 = 0.0;
     int e = 0;
-    if (h0 > 0) {  // wide (h0 = ne) / split layouts: entries [0, h0) in order, then [h0, ne)
+    if (h0 > 0) {  // entries [0, h0) in order, then [h0, ne) (wide layout: h0 = ne)
       for (; e + 8 <= ne; e += 8) {
         double x[8];
 #pragma unroll
@@ -1442,11 +1123,9 @@ hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx
 }
 
 // where the layout of basis length nv splits its update sum in two (0: the pair layout's even /
-// odd entries): the whole sum for the wide layout, half 0's entries for the split layout
-// (non-augmentation steps: the edge kernel only sums for those)
+// odd entries; nv + 1: the wide layout's whole sum in entry order)
 int edge_split_point(int nv) {
   if (arnoldi_wide(nv)) return nv + 1;
-  if (arnoldi_split(nv)) return (nv + 3) / 2;
   return 0;
 }
 
@@ -1460,11 +1139,6 @@ hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) 
 bool arnoldi_wide(int nv) {
   static const bool on = env_int("NKHIP_ARN_WIDE", 1) != 0;
   return on && nv <= kWideMaxNV;
-}
-
-bool arnoldi_split(int nv) {
-  static const bool on = env_int("NKHIP_ARN_SPLIT", 1) != 0;
-  return on && nv > kWideMaxNV && nv <= kSplitMaxNV;
 }
 
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx) {

@@ -192,26 +192,7 @@ __global__ void __launch_bounds__(RB) reduce_final_kernel(const double* partial,
                                                           int nsum, double* result,
                                                           double* result_host) {
   const int k = blockIdx.x;
-  const bool is_sum = k < nsum;
-  const double* p = partial + int64_t(k) * nblk;
-  // max reductions start from -inf (signed quantities such as -min(...) are allowed); the
-  // loads of one thread are issued together (no dependent load chain)
-  double acc = is_sum ? 0.0 : -INFINITY;
-  int64_t b = threadIdx.x;
-  for (; b + 3 * RB < nblk; b += 4 * RB) {
-    const double x0 = p[b], x1 = p[b + RB], x2 = p[b + 2 * RB], x3 = p[b + 3 * RB];
-    acc = is_sum ? acc + x0 + x1 + x2 + x3 : nmax(nmax(nmax(nmax(acc, x0), x1), x2), x3);
-  }
-  for (; b < nblk; b += RB) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
-  double v[1] = {acc};
-  // the reduction tree is fixed, so the result does not depend on timing
-  double s = 0.0;
-  if (is_sum) {
-    s = block_reduce<1, 1, RB>(v);
-  } else {
-    s = block_reduce<1, 0, RB>(v);
-  }
-  if (nblk == 0) s = 0.0;  // empty input
+  const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, k < nsum);
   if (threadIdx.x == 0) {
     result[k] = s;
     if (result_host) result_host[k] = s;  // pinned, device-mapped host memory: no D2H blit

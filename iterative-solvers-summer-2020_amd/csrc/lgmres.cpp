@@ -18,6 +18,14 @@
 // the last one, the JVP/multi-dot issued for j+1 are discarded (not counted).
 // NKHIP_LAGNORM=0 disables the lagged norm (every step reduces |v_{j+1}| first); so does a
 // problem that must not evaluate a discarded JVP (a user callback: scipy's exact F-call count).
+//
+// Device-side control (device_steps, arnctl.hip): once a fused step applies J to the new basis
+// vector itself, the same per-step arithmetic runs in a one-wave kernel between the fused
+// launches and the host only queues launches ahead of it; the kernel hands the step that ends
+// the process (or that needs a path it does not take) back to this loop.  NKHIP_DEVCTL=1/0
+// forces it on/off (default: on with a communicator, see devctl_enabled).
+#include <atomic>
+#include <cstddef>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -31,6 +39,17 @@ namespace {
 constexpr double kEps = DBL_EPSILON;
 constexpr double kLagMinRatio2 = 1e-12;  // (|v|_est / |w|)^2 below which the estimate is not used
 
+// Default: on with a communicator, where the host path waits for a stream synchronisation after
+// every all-reduce; off on one GPU, where polling the pinned result slots already costs only the
+// ~6-12 us between two launches and the device path measured 0.5-0.9 % slower (its entry and
+// hand-back launches per LGMRES call outweigh the ~5 us it saves per step).  Read per call.
+bool devctl_enabled(bool multi) {
+  const char* v = std::getenv("NKHIP_DEVCTL");
+  if (v && v[0] == '0') return false;
+  if (v && v[0] == '1') return true;
+  return multi;
+}
+
 bool lag_enabled() {
   static const bool on = [] {
     const char* v = std::getenv("NKHIP_LAGNORM");
@@ -43,7 +62,7 @@ bool lag_enabled() {
 int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bool dev_scale) {
   const int64_t n = E_.n;
   zp_[j] = z;
-  zs_[j] = zs;  // provisional when the exact scale of z is only known later
+  hS_->zs[j] = zs;  // provisional when the exact scale of z is only known later
   double* w = V_[j + 1];
   int rc;
   if (dev_scale) {  // z = raw basis vector whose |z|^2 the combo left in device memory
@@ -68,7 +87,7 @@ int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bo
                  [&] { return mdot_launch(w, g, P, j + 1, n, E_.partial(), E_.s, &nblk); });
   if (rc) return rc;
   const int np = j + 1;
-  return E_.reduce_async(nblk, 2 * np + 1, 2 * np + 1, Engine::kSlotMdot);
+  return E_.reduce_async(nblk, 2 * np + 1, 2 * np + 1, Engine::slot_mdot(j));
 }
 
 int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec) {
@@ -88,16 +107,28 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   const int64_t n = E_.n;
   const int K = int(outer_.size());
   const bool lag = lag_enabled() && P_.may_speculate();
+  const bool devctl = lag && devctl_enabled(E_.comm != nullptr);
   V_[0] = Fx_;  // v0 = b / |b|, kept raw with scale 1/|b|
-  double sig[kMaxVec + 2], rn[kMaxVec + 2], sig_est[kMaxVec + 2], wnorm[kMaxVec + 2];
+  // the loop state (shared with the device-side control: nk_kernels.h ArnCtlState)
+  ArnCtlState& S = *hS_;
+  S.m = m;
+  S.halt = 0;
+  S.steps = 0;
+  S.ptol = ptol;
+  S.omega = omega_;
+  S.lag_ratio2 = kLagMinRatio2;
+  double* const sig = S.sig;
+  double* const rn = S.rn;
+  double* const sig_est = S.sig_est;
+  double* const wnorm = S.wnorm;
+  double* const zs_ = S.zs;
+  double* const h = S.h;
   sig[0] = 1.0 / b_norm;
   rn[0] = b_norm;
-  static thread_local double R[kMaxVec + 1][kMaxVec + 1];
-  static thread_local double gram[kMaxVec + 1][kMaxVec + 1];
-  double cs[kMaxVec + 1], sn[kMaxVec + 1], gv[kMaxVec + 2], hcur[kMaxVec + 2], h[kMaxVec + 1];
+  double hcur[kMaxVec + 2];
   double red[2 * kMaxVec + 2];
-  for (int i = 0; i < kMaxVec + 2; ++i) gv[i] = 0.0;
-  gv[0] = 1.0;
+  for (int i = 0; i < kMaxVec + 2; ++i) S.gv[i] = 0.0;
+  S.gv[0] = 1.0;
 
   // input of step j whose scale is known on the host: the augmentation vectors first
   // (_gcrotmk.py:107-110), then v0 (:111-113), then the newest basis vector (:117-118)
@@ -116,6 +147,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   };
   // Step i is complete once hn = |v_{i+1}| (raw) is known: Hessenberg column i, Givens update of
   // its QR (qr_insert, _gcrotmk.py:146-158), residual test (:165).  True when the process stops.
+  // (arnctl.hip restates this for the device-side control.)
   auto finish = [&](int i, double hn) -> bool {
     for (int k = 0; k <= i; ++k) hcur[k] = h[k];
     hcur[i + 1] = hn;
@@ -124,16 +156,16 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     rn[i + 1] = hn;
     const bool breakdown = !(hn > kEps * wnorm[i]);
     for (int k = 0; k < i; ++k) {
-      const double t = cs[k] * hcur[k] + sn[k] * hcur[k + 1];
-      hcur[k + 1] = -sn[k] * hcur[k] + cs[k] * hcur[k + 1];
+      const double t = S.cs[k] * hcur[k] + S.sn[k] * hcur[k + 1];
+      hcur[k + 1] = -S.sn[k] * hcur[k] + S.cs[k] * hcur[k + 1];
       hcur[k] = t;
     }
-    detail::givens(hcur[i], hcur[i + 1], &cs[i], &sn[i]);
-    hcur[i] = cs[i] * hcur[i] + sn[i] * hcur[i + 1];
-    for (int k = 0; k <= i; ++k) R[k][i] = hcur[k];
-    gv[i + 1] = -sn[i] * gv[i];
-    gv[i] = cs[i] * gv[i];
-    return std::fabs(gv[i + 1]) < ptol || breakdown;
+    detail::givens(hcur[i], hcur[i + 1], &S.cs[i], &S.sn[i]);
+    hcur[i] = S.cs[i] * hcur[i] + S.sn[i] * hcur[i + 1];
+    for (int k = 0; k <= i; ++k) S.R[k][i] = hcur[k];
+    S.gv[i + 1] = -S.sn[i] * S.gv[i];
+    S.gv[i] = S.cs[i] * S.gv[i];
+    return std::fabs(S.gv[i + 1]) < ptol || breakdown;
   };
 
   int rc;
@@ -151,7 +183,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   for (;;) {
     // -- results of the multi-dot of step j
     const int np = j + 1;
-    std::memcpy(red, E_.hres(Engine::kSlotMdot), sizeof(double) * (2 * np + 1));
+    std::memcpy(red, E_.hres(Engine::slot_mdot(j)), sizeof(double) * (2 * np + 1));
     double tau = 1.0;
     if (hn_pending) {
       hn_pending = false;
@@ -169,12 +201,12 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     const double ww = tau * tau * red[2 * np];
     if (!std::isfinite(ww)) return NK_NONFINITE;  // _nonlin.py:1511-1512
     wnorm[j] = std::sqrt(ww);
-    for (int i = 0; i < j; ++i) gram[j][i] = sig[j] * sig[i] * red[np + i];
+    for (int i = 0; i < j; ++i) S.gram[j][i] = sig[j] * sig[i] * red[np + i];
     // MGS coefficients from the Gram matrix: (I + L) h = V^T w (inverse compact WY form)
     double hh = 0.0;
     for (int i = 0; i <= j; ++i) {
       double acc = tau * sig[i] * red[i];
-      for (int k = 0; k < i; ++k) acc -= gram[i][k] * h[k];
+      for (int k = 0; k < i; ++k) acc -= S.gram[i][k] * h[k];
       h[i] = acc;
       hh += acc * acc;
     }
@@ -211,7 +243,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
         int64_t nw = 0;
         double* vout = Sv_;
         rc = P_.fused_step(Vp, cc, j + 1, w, tau, X_, G0_, z, zs, omega_ / zn, vout, V_[j + 2],
-                           &nw);
+                           &nw, nullptr);
         if (rc) return rc;
         Sv_ = V_[j + 1];
         V_[j + 1] = vout;
@@ -221,11 +253,20 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
         st_->njvp += 1;
         st_->n_arnoldi += 1;
         const int np1 = j + 2;
-        rc = E_.reduce_async(nw, 2 * np1 + 1, 2 * np1 + 1, Engine::kSlotMdot);
-        if (!rc) rc = E_.wait_results(Engine::kSlotMdot, 2 * np1 + 1);
+        rc = E_.reduce_async(nw, 2 * np1 + 1, 2 * np1 + 1, Engine::slot_mdot(j + 1));
         if (rc) return rc;
         hn_pending = true;
         ++j;
+        if (devctl && next_is_v) {  // the following steps: device-side control
+          S.j = j;
+          S.hn_pending = 1;
+          rc = device_steps();
+          j = S.j;
+          hn_pending = S.hn_pending != 0;
+        } else {
+          rc = E_.wait_results(Engine::slot_mdot(j), 2 * np1 + 1);
+        }
+        if (rc) return rc;
         continue;
       }
     }
@@ -293,9 +334,9 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     ++j;
   }
   j = last;
-  if (!std::isfinite(R[j][j])) return NK_OK;  // LinAlgError -> lgmres returns x = 0
+  if (!std::isfinite(S.R[j][j])) return NK_OK;  // LinAlgError -> lgmres returns x = 0
   double y[kMaxVec + 1];
-  detail::lstsq_upper(R, j + 1, gv, y);
+  detail::lstsq_upper(S.R, j + 1, S.gv, y);
   for (int i = 0; i <= j; ++i) {
     y[i] *= b_norm;  // y *= inner_res_0
     if (!std::isfinite(y[i])) return NK_OK;
@@ -329,6 +370,97 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   *dnorm = nx;
   *dmax = r2[1];
   *dvec = d;
+  return NK_OK;
+}
+
+int NewtonKrylov::device_steps() {
+  ArnCtlState& S = *hS_;
+  const int t0 = S.j;
+  // the largest basis length the device issues fused steps for (every length up to it runs fused)
+  int nvmax = t0;
+  while (nvmax + 1 < S.m && nvmax + 1 <= kArnMaxNV && P_.has_fused(nvmax + 1)) ++nvmax;
+  if (nvmax < t0 + 1) return E_.wait_results(Engine::slot_mdot(t0), 2 * (t0 + 1) + 1);
+  S.nv_max = nvmax;
+  S.halt = 0;
+  S.steps = 0;
+  S.arrive = 0;
+  volatile uint32_t* st = status_;
+  for (int t = t0; t < S.m && t < kMaxVec + 2; ++t) st[t] = 0;
+  std::atomic_thread_fence(std::memory_order_release);
+  // the state the control reads: everything before R, and the Gram rows of the earlier steps.
+  // From here the device writes every committed value into hS_ as well (no read-back).
+  if (hipMemcpyAsync(dS_, hS_, offsetof(ArnCtlState, R), hipMemcpyHostToDevice, E_.s) !=
+          hipSuccess ||
+      (t0 > 0 && hipMemcpyAsync(&dS_->gram[0][0], &S.gram[0][0], sizeof(S.gram[0]) * t0,
+                                hipMemcpyHostToDevice, E_.s) != hipSuccess))
+    return NK_EHIP;
+
+  const bool one = E_.comm == nullptr;  // no all-reduce: the reduction carries the control
+  struct Rot {
+    double* spare;
+    double* v;
+    bool fused;
+  };
+  Rot rot[kMaxVec + 2];
+  double cc[kMaxVec] = {};  // the launch arguments the parameter block overrides
+  // the control of step t on the (all-reduced) multi-dot results in its slot
+  auto control = [&](int t) {
+    return E_.launch(K_CTL, 0.0, [&] {
+      return arn_ctl_launch(dS_, hS_, E_.dres(Engine::slot_mdot(t)), prm_, status_, t, E_.s);
+    });
+  };
+  // the fused step nv = t + 1 with the parameters control t writes, its reduction into the slot
+  // of step t + 1 and the control of step t + 1
+  auto issue = [&](int t) -> int {
+    rot[t] = Rot{Sv_, V_[t + 1], false};
+    const double* Vp[kMaxVec];
+    for (int i = 0; i <= t; ++i) Vp[i] = V_[i];
+    double* vout = Sv_;
+    int64_t nw = 0;
+    int rc = P_.fused_step(Vp, cc, t + 1, V_[t + 1], 1.0, X_, G0_, nullptr, 1.0, 1.0, vout,
+                           V_[t + 2], &nw, prm_);
+    if (rc) return rc;
+    Sv_ = V_[t + 1];
+    V_[t + 1] = vout;
+    zp_[t + 1] = vout;
+    rot[t].fused = true;
+    const int nval = 2 * (t + 2) + 1;
+    const int slot = Engine::slot_mdot(t + 1);
+    if (one)
+      return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
+        return arn_reduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
+                                     E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
+      });
+    rc = E_.reduce_async(nw, nval, nval, slot);
+    return rc ? rc : control(t + 1);
+  };
+  // one fused step queued beyond the one whose control is awaited, so the stream never waits
+  // for the host; a step handed back leaves at most one launch pair behind that does nothing
+  int rc = control(t0);
+  int next = t0;  // the next fused step to queue
+  if (!rc) rc = issue(next++);
+  int t = t0;
+  while (!rc) {
+    const uint32_t v = E_.wait_flag(status_ + t);
+    if (v != 1) {
+      if (v != 2) rc = NK_EHIP;  // the control of step t never ran
+      break;
+    }
+    st_->njvp += 1;  // step t's fused step is part of the process
+    st_->n_arnoldi += 1;
+    st_->n_device_steps += 1;
+    ++t;
+    if (next == t && next + 1 <= nvmax) rc = issue(next++);
+  }
+  // step t was handed back: the fused steps queued from t on do nothing; undo their rotations
+  for (int u = next - 1; u >= t; --u) {
+    if (!rot[u].fused) continue;
+    Sv_ = rot[u].spare;
+    V_[u + 1] = rot[u].v;
+  }
+  if (rc) return rc;
+  if (S.j != t || S.halt != 1 + t) return NK_EHIP;
+  S.halt = 0;
   return NK_OK;
 }
 

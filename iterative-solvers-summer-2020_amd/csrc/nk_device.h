@@ -56,4 +56,23 @@ __device__ __forceinline__ double block_reduce(double (&v)[NV], int buf = 0) {
   return acc;
 }
 
+// One column of a partial-sum matrix reduced by a block of RB threads: the sum (or NaN-propagating
+// max) of p[0 .. nblk), in a fixed tree (the result does not depend on timing).  Thread 0's
+// return value is the result.
+template <int RB>
+__device__ __forceinline__ double reduce_column(const double* p, int64_t nblk, bool is_sum) {
+  // max reductions start from -inf (signed quantities such as -min(...) are allowed); the
+  // loads of one thread are issued together (no dependent load chain)
+  double acc = is_sum ? 0.0 : -INFINITY;
+  int64_t b = threadIdx.x;
+  for (; b + 3 * RB < nblk; b += 4 * RB) {
+    const double x0 = p[b], x1 = p[b + RB], x2 = p[b + 2 * RB], x3 = p[b + 3 * RB];
+    acc = is_sum ? acc + x0 + x1 + x2 + x3 : nmax(nmax(nmax(nmax(acc, x0), x1), x2), x3);
+  }
+  for (; b < nblk; b += RB) acc = is_sum ? acc + p[b] : nmax(acc, p[b]);
+  double v[1] = {acc};
+  const double s = is_sum ? block_reduce<1, 1, RB>(v) : block_reduce<1, 0, RB>(v);
+  return (nblk == 0) ? 0.0 : s;  // empty input
+}
+
 }  // namespace nk

@@ -164,16 +164,65 @@ struct ArnoldiArgs {
   bool plan_only = false;          // set *nwaves only, launch nothing
   int reserve_cus = 0;             // size the grid to leave this many CUs free (a concurrent
                                    // halo exchange needs CUs for its kernels)
+  // device-side Arnoldi control (arn_ctl_launch): c, tau, alpha, sc come from the parameter block
+  // ctl[kCtlPrm] the control kernel wrote instead of the fields above, and the launch does
+  // nothing when its halt entry is set (the control handed the loop back to the host)
+  const double* ctl = nullptr;
 };
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // basis length nv runs the wide layout (128-column waves, 512-column blocks; NKHIP_ARN_WIDE=0: off)
 bool arnoldi_wide(int nv);
-// basis length nv runs the split layout (128-column waves, entry halves on two waves; NKHIP_ARN_SPLIT=0: off)
-bool arnoldi_split(int nv);
 // *nwaves = partial columns written: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']
 hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
 // u = v (or z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
 // with the fused kernel's summation order: what the neighbours need as their halo rows
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Device-side Arnoldi control (arnctl.hip, lgmres.cpp).  The loop state of one LGMRES call: the
+// host loop works on it in pinned memory, and hands it to the device (one copy) for runs of
+// fused steps whose control -- Givens update of the previous Hessenberg column, residual test,
+// Gram row, MGS coefficients, the lagged norm of the next vector -- a one-wave kernel computes
+// between the fused launches, so no host round trip separates two Arnoldi steps.  Whatever the
+// kernel does not handle (the stop, a cancelling norm estimate, a non-finite |w|) it hands back:
+// it leaves the state as it was before that step and sets `halt`.
+struct ArnCtlState {
+  int32_t j;           // the step whose multi-dot results are consumed next
+  int32_t hn_pending;  // step j - 1 still waits for |v_j| (the Gram diagonal of those results)
+  int32_t m;           // steps of this call (inner_m + augmentation vectors)
+  int32_t nv_max;      // the device issues fused steps up to this basis length
+  int32_t halt;        // 0: the device continues; else 1 + the step it handed back
+  int32_t steps;       // steps the device completed
+  uint32_t arrive;     // blocks of the running reduction that finished (arn_reduce_ctl_launch)
+  int32_t pad_;
+  double ptol, omega, lag_ratio2, pad2_;
+  double sig[kMaxVec + 2];      // scale of basis vector i (kept raw: v_i = sig_i V_i)
+  double rn[kMaxVec + 2];       // |V_i| raw
+  double sig_est[kMaxVec + 2];  // the lagged scale JVP_i saw (0: exact)
+  double wnorm[kMaxVec + 2];    // |w_i|
+  double zs[kMaxVec + 2];       // scale of the JVP input z_i (the final combination)
+  double cs[kMaxVec + 1], sn[kMaxVec + 1];  // Givens rotations of the Hessenberg QR
+  double gv[kMaxVec + 2];       // rotated right-hand side (residual estimate gv[j+1])
+  double h[kMaxVec + 2];        // MGS coefficients of the latest step
+  double R[kMaxVec + 1][kMaxVec + 1];
+  double gram[kMaxVec + 1][kMaxVec + 1];  // sig_i sig_k (V_i . V_k), k < i
+};
+// parameter block of one fused step the control kernel writes: c[0..kArnMaxNV), tau, alpha, sc,
+// halt (non-zero: the step was handed back, the queued launches do nothing)
+constexpr int kCtlPrm = kArnMaxNV + 4;
+// Control of step t (== S->j): consumes the all-reduced multi-dot results `red` of step t and,
+// if the device continues, writes the parameters of the fused step with nv = t + 1 to prm and
+// advances S.  Every committed value is also written to H, the host's pinned copy of the state,
+// so the host needs no read-back when the device hands a step back.  status[t] (pinned host
+// memory) <- 1 (continued) or 2 (handed back) after those writes.  Nothing runs once S->halt is
+// set.
+hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* prm,
+                          uint32_t* status, int t, hipStream_t s);
+// The same preceded by the reduction of the fused step's partials (one GPU: no all-reduce in
+// between) in one launch: result[k] = sum_b partial[k nblk + b] for k < nval (and result_host,
+// pinned), then the last block to finish runs the control of step t on result.
+hipError_t arn_reduce_ctl_launch(const double* partial, int64_t nblk, int nval, double* result,
+                                 double* result_host, ArnCtlState* S, ArnCtlState* H, double* prm,
+                                 uint32_t* status, int t, hipStream_t s);
 
 }  // namespace nk

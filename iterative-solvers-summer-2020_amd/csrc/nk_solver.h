@@ -41,6 +41,7 @@ enum Kind : int {
   K_ARN_EDGE,
   K_EDGE,
   K_ARN_SLAB,
+  K_CTL,
   K_NKINDS
 };
 
@@ -106,16 +107,23 @@ class Engine {
   int reduce_async(int64_t nblk, int nsum, int nv, int slot);
   const double* dres(int slot) const { return dres_ + slot; }
   const double* hres(int slot) const { return hres_ + slot; }
-  static constexpr int kSlots = 512;
-  static constexpr int kSlotMdot = 0;     // <= 2*kMaxVec+1 values
-  static constexpr int kSlotCombo = 256;  // 2 values
-  static constexpr int kSlotSync = 384;   // reduce()
+  double* dres_mut(int slot) const { return dres_ + slot; }  // for a kernel that writes a slot
+  double* hres_mut(int slot) const { return hres_ + slot; }
+  static constexpr int kSlots = 1024;
+  // multi-dot results of Arnoldi step j (<= 2*kMaxVec+1 values): a ring of four, so the results
+  // of a step stay readable while the device-side control queues the next two
+  static int slot_mdot(int j) { return (j & 3) * 136; }
+  static constexpr int kSlotCombo = 560;  // 2 values
+  static constexpr int kSlotSync = 600;   // reduce()
   int sync();
   // Wait for the nv results a reduce_async(.., slot) writes to the pinned host slots, by polling
   // them (the reduction kernel stores every value straight into pinned memory, the slots were
   // marked beforehand); no stream synchronisation.  Falls back to sync() with a communicator
   // (results come through a D2H copy), after ~1 s, or with NKHIP_POLL=0.
   int wait_results(int slot, int nv);
+  // Wait until a kernel sets the pinned word *flag (non-zero); returns its value, or 0 after a
+  // stream synchronisation found it still unset (the writer did not run).
+  uint32_t wait_flag(const uint32_t* flag);
   int copy(double* dst, const double* src, int64_t n);
 
   double* partial() const { return partial_; }
@@ -203,9 +211,12 @@ struct Problem {
   virtual int fused_step(const double* const* /*V*/, const double* /*c*/, int /*nv*/,
                          const double* /*w*/, double /*tau*/, const double* /*x0*/,
                          const double* /*G0*/, const double* /*z*/, double /*zs*/, double /*sc*/,
-                         double* /*out_v*/, double* /*out_w*/, int64_t* /*nwaves*/) {
+                         double* /*out_v*/, double* /*out_w*/, int64_t* /*nwaves*/,
+                         const double* /*ctl*/) {
     return NK_EINVAL;
   }
+  // ctl of fused_step (device-side Arnoldi control, nk_kernels.h ArnoldiArgs): c, tau, zs and sc
+  // come from the device parameter block ctl, and the step does nothing when its halt entry is set.
   // v (a pool vector) may enter the update of a later fused step: refresh its edge array
   virtual int publish_edges(const double* /*v*/) { return NK_OK; }
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
@@ -217,6 +228,9 @@ class NewtonKrylov {
  public:
   NewtonKrylov(Engine& E, Problem& P, const nk_opts& o, void* external = nullptr,
                int64_t external_bytes = 0);
+  ~NewtonKrylov();
+  NewtonKrylov(const NewtonKrylov&) = delete;
+  NewtonKrylov& operator=(const NewtonKrylov&) = delete;
   int status() const { return init_status_; }
   void set_opts(const nk_opts& o) { o_ = o; }
   // x_out = root of F starting from x_in (device, length n; may alias).  Returns NK_* status.
@@ -227,8 +241,16 @@ class NewtonKrylov {
   int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
   // Launch JVP_j (w = V[j+1] = J z_j) and the fused multi-dot of step j; no synchronisation.
   int issue_step(int j, const double* z, double zs, double znorm, bool dev_scale);
+  // Device-side Arnoldi control (arnctl.hip): from step S.j (whose fused launch and reduction
+  // are queued), queue fused step + reduction + control per step, one step ahead of the
+  // control's status words, until the control hands a step back; then restore the host's view
+  // of the vectors at that step (the control mirrors the state into hS_ itself).
+  int device_steps();
   const double* zp_[kMaxVec + 1];
-  double zs_[kMaxVec + 1];
+  ArnCtlState* hS_ = nullptr;   // the loop state (pinned; zs_ of the final combination inside)
+  ArnCtlState* dS_ = nullptr;   // its device copy
+  double* prm_ = nullptr;       // parameter block of the next fused step (device)
+  uint32_t* status_ = nullptr;  // per-step status words the control kernel writes (pinned)
   int line_search(double* s_out, double* fnorm_new, double* fmax, double* xmax);
 
   Engine& E_;

@@ -229,8 +229,10 @@ bool SHProblem::has_fused(int nv) const {
 
 int SHProblem::fused_step(const double* const* V, const double* c, int nv, const double* w,
                           double tau, const double* x0, const double* G0, const double* z,
-                          double zs, double sc, double* out_v, double* out_w, int64_t* nwaves) {
+                          double zs, double sc, double* out_v, double* out_w, int64_t* nwaves,
+                          const double* ctl) {
   ArnoldiArgs A;
+  A.ctl = ctl;
   A.ny = ny_;
   A.nx = nx_;
   A.nv = nv;
@@ -254,7 +256,8 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   bool all = true;
   for (int i = 0; i < nv; ++i) all = all && (A.E[i] = E_.edges(V[i])) != nullptr;
   all = all && (A.E[nv] = E_.edges(w)) != nullptr;
-  if (!all || std::getenv("NKHIP_EDGES") && std::getenv("NKHIP_EDGES")[0] == '0')
+  const char* eoff = std::getenv("NKHIP_EDGES");
+  if (!all || (eoff && eoff[0] == '0'))
     for (int i = 0; i <= nv; ++i) A.E[i] = nullptr;
   A.Eout_v = E_.edges(out_v);
   A.Eout_w = E_.edges(out_w);

@@ -36,7 +36,7 @@ class nk_stats(C.Structure):
     _fields_ = [("nit", C.c_int64), ("nfev", C.c_int64), ("njvp", C.c_int64),
                 ("n_arnoldi", C.c_int64), ("fnorm_inf", C.c_double), ("fnorm_2", C.c_double),
                 ("status", C.c_int32), ("pad_", C.c_int32), ("n_backtrack", C.c_int64),
-                ("step_min", C.c_double)]
+                ("step_min", C.c_double), ("n_device_steps", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad_"}

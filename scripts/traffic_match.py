@@ -27,8 +27,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def klass(name):
     k = name.replace("void ", "").replace("nk::(anonymous namespace)::", "")
-    if k.startswith("arnoldi_kernel<"):
+    if k.startswith("arnoldi_kernel<") or k.startswith("arnoldi_wide_kernel<"):
         return "arnoldi_fused"
+    if k.startswith("arn_ctl_kernel") or k.startswith("arn_reduce_ctl_kernel"):
+        return "arnoldi_ctl"
+    if k.startswith("edge_gather_kernel"):
+        return "edge_gather"
     if k.startswith("arnoldi_edge_kernel"):
         return "arnoldi_edge"
     if k.startswith("combo_kernel<"):

@@ -119,24 +119,28 @@ def test_fused_kernel_vs_torch(ny, nx, nv, ext):
         assert abs(a - b) <= 1e-10 * scale, (i, a, b)
 
 
+@pytest.mark.parametrize("devctl", ["1", "0"])
 @pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("nranks,ny_total,nx", [(2, 64, 64), (3, 96, 130), (4, 48, 40),
                                                   (8, 1024, 1024)])
-def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, monkeypatch):
+def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, devctl, monkeypatch):
     """Row slabs through the fused kernel: every rank evaluates y on its edge rows, the loopback
     communicator exchanges them (the RCCL path's protocol), and the fused pass takes them as its
-    halo rows.  Same root as the single periodic slab, and the fused kernel did run on each slab."""
+    halo rows.  Same root as the single periodic slab, and the fused kernel did run on each slab.
+    devctl "1" (the default with a communicator): the Arnoldi control runs on the device, every
+    rank's control kernel taking the same decisions from the same all-reduced results."""
     import nkhip
     from conftest import run_slabs
     # "1": interior rows on a side stream during the edge exchange, edge bands after it
     monkeypatch.setenv("NKHIP_SLAB_OVERLAP", overlap)
+    monkeypatch.setenv("NKHIP_DEVCTL", devctl)
     U0 = np.random.default_rng(7).standard_normal((ny_total, nx))
     single = nkhip.SwiftHohenberg(N=nx, ny=ny_total, d=0.625 * nx, f_tol=1e-10)
     ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
     ref_nit = single.last_stats["nit"]
     single.close()
     comms = nkhip.loopback_comms(nranks)
-    out, profs, nits = [None] * nranks, [None] * nranks, [None] * nranks
+    out, profs, nits, devs = [None] * nranks, [None] * nranks, [None] * nranks, [None] * nranks
 
     def run(p):
         stream = torch.cuda.Stream()
@@ -147,6 +151,7 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, monkeypatc
             u = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
             out[p] = m.step(u).cpu().numpy()
             nits[p] = m.last_stats["nit"]
+            devs[p] = m.last_stats["n_device_steps"]
             profs[p] = m.kernel_profile()
             stream.synchronize()
             m.close()
@@ -158,6 +163,7 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, monkeypatc
         if overlap == "1" and ny_total // nranks >= 12:
             assert pr["arnoldi_slab_edges"]["launches"] == pr["arnoldi_fused"]["launches"]
     assert len(set(nits)) == 1 and abs(nits[0] - ref_nit) <= 1
+    assert len(set(devs)) == 1 and ((devs[0] > 0) == (devctl == "1")), devs
     got = np.concatenate(out, axis=0)
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
     F = sh_oracle.residual(got.reshape(-1), U0.reshape(-1), ny_total, nx, 0.625, 0.01, 0.2, 1.0)
@@ -199,3 +205,38 @@ def test_edges_identical_solve(ny, nx, monkeypatch):
     _, b, sb, pb = _step(ny, nx, fused=True)
     assert np.array_equal(a, b) and sa == sb
     assert pb["edge_gather"]["launches"] > 0 and pb["arnoldi_fused"]["launches"] > 0
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 64), (128, 60), (96, 130), (256, 256), (40, 512)])
+def test_device_control_matches_host(ny, nx, monkeypatch):
+    """Device-side Arnoldi control (arnctl.hip: the Givens update, residual test, Gram row and
+    MGS coefficients computed by a one-wave kernel between the fused launches, handed back to the
+    host loop at the stop): the same root as the host loop to 1e-8 of the state's scale, Newton
+    counts within one, a root of the oracle residual, and the device did run steps."""
+    monkeypatch.setenv("NKHIP_DEVCTL", "0")
+    U0, a, sa, _ = _step(ny, nx, fused=True, steps=2)
+    monkeypatch.setenv("NKHIP_DEVCTL", "1")
+    _, b, sb, pb = _step(ny, nx, fused=True, steps=2)
+    assert all(s["n_device_steps"] == 0 for s in sa)
+    assert sum(s["n_device_steps"] for s in sb) > 0
+    assert pb["arnoldi_ctl"]["launches"] > 0
+    for x, y in zip(sa, sb):
+        assert abs(x["nit"] - y["nit"]) <= 1 and y["status"] == 0
+        # the device steps are a subset of the Arnoldi steps
+        assert y["n_device_steps"] < y["n_arnoldi"]
+    assert np.abs(a - b).max() <= 1e-8 * max(1.0, np.abs(a).max())
+
+
+def test_device_control_default_tolerance():
+    """At scipy's default f_tol the device-controlled solve reaches a root of the oracle
+    residual with the host loop's Newton count (within one), over several time steps."""
+    ny = nx = 128
+    os.environ["NKHIP_DEVCTL"] = "1"
+    try:
+        U0, b, sb, _ = _step(ny, nx, fused=True, ftol=None, steps=1)
+    finally:
+        os.environ.pop("NKHIP_DEVCTL", None)
+    _, a, sa, _ = _step(ny, nx, fused=True, ftol=None, steps=1)
+    assert abs(sa[0]["nit"] - sb[0]["nit"]) <= 1 and sb[0]["n_device_steps"] > 0
+    F = sh_oracle.residual(b.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
+    assert np.abs(F).max() <= 1.01 * np.finfo(float).eps ** (1 / 3)
