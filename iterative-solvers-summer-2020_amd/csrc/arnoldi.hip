@@ -115,7 +115,9 @@ __device__ __forceinline__ bool arn_halted(const ArnoldiArgs& A) {
 
 // Rows of loads in flight per wave for a basis of NV vectors (register budget at one or two
 // waves per SIMD; the wait counter tracks at most 63 loads)
-constexpr int pf_for(int nv) { return nv <= 4 ? 3 : nv <= 20 ? 2 : 1; }
+// (the pair layout runs nv >= 19, where one row in flight measured 2 % faster than two at nv 19-20:
+// profiles/r02_arnoldi_ab.md)
+constexpr int pf_for(int nv) { return nv <= 4 ? 3 : nv <= 18 ? 2 : 1; }
 
 __device__ __forceinline__ double readlane(double v, int l) {
   const u32x2 b = __builtin_bit_cast(u32x2, v);
