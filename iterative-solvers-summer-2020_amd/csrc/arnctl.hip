@@ -29,8 +29,8 @@ __device__ __forceinline__ double bcast(double v, int l) {  // lane l's v, l wav
 
 // The control of step t, run by the first wave of a block (the other waves of the block must not
 // take part).  S: device state, H: the host's pinned copy (committed values go to both).
-__device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, double* prm,
-                         uint32_t* status, int t) {
+__device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
+                         double* prm, uint32_t* status, int t) {
   const int lane = threadIdx.x & 63;
   // the same field of H as p of S
   auto mirror = [&](auto* p) {
@@ -58,6 +58,9 @@ __device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, doub
   const double se = S->sig_est[j], ptol = S->ptol, omega = S->omega, lr2 = S->lag_ratio2;
   const int32_t steps = S->steps;
   if (halted) return;  // an earlier step was handed back: the host takes over from there
+  if (red_host) {  // the results of step t for the host (read if this step is handed back)
+    for (int i = lane; i <= 2 * np; i += 64) red_host[i] = red[i];
+  }
   // hand step j back to the host unchanged (the host loop redoes it from the same state)
   auto hand_back = [&] {
     if (lane == 0) {
@@ -174,9 +177,9 @@ __device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, doub
 }
 
 __global__ void __launch_bounds__(64) arn_ctl_kernel(ArnCtlState* S, ArnCtlState* H,
-                                                     const double* red, double* prm,
-                                                     uint32_t* status, int t) {
-  ctl_body(S, H, red, prm, status, t);
+                                                     const double* red, double* red_host,
+                                                     double* prm, uint32_t* status, int t) {
+  ctl_body(S, H, red, red_host, prm, status, t);
 }
 
 __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partial, int64_t nblk,
@@ -196,15 +199,16 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
   if (!last || threadIdx.x >= 64) return;
   __threadfence();  // every other block's result is visible after its arrival
   if (threadIdx.x == 0) S->arrive = 0;  // for the next launch (stream order)
-  ctl_body(S, H, result, prm, status, t);
+  ctl_body(S, H, result, nullptr, prm, status, t);
 }
 
 }  // namespace
 
-hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* prm,
-                          uint32_t* status, int t, hipStream_t s) {
+hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
+                          double* prm, uint32_t* status, int t, hipStream_t s) {
   if (!S || !H || !red || !prm || !status || t < 0 || t > kMaxVec) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(arn_ctl_kernel, dim3(1), dim3(64), 0, s, S, H, red, prm, status, t);
+  hipLaunchKernelGGL(arn_ctl_kernel, dim3(1), dim3(64), 0, s, S, H, red, red_host, prm, status,
+                     t);
   return hipGetLastError();
 }
 

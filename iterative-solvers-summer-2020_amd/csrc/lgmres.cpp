@@ -404,9 +404,13 @@ int NewtonKrylov::device_steps() {
   Rot rot[kMaxVec + 2];
   double cc[kMaxVec] = {};  // the launch arguments the parameter block overrides
   // the control of step t on the (all-reduced) multi-dot results in its slot
-  auto control = [&](int t) {
+  // the control of step t on the (all-reduced) multi-dot results in its slot; `copy`: the
+  // results also to the host slot (the all-reduce path leaves out its own D2H copy)
+  auto control = [&](int t, bool copy) {
+    const int slot = Engine::slot_mdot(t);
     return E_.launch(K_CTL, 0.0, [&] {
-      return arn_ctl_launch(dS_, hS_, E_.dres(Engine::slot_mdot(t)), prm_, status_, t, E_.s);
+      return arn_ctl_launch(dS_, hS_, E_.dres(slot), copy ? E_.hres_mut(slot) : nullptr, prm_,
+                            status_, t, E_.s);
     });
   };
   // the fused step nv = t + 1 with the parameters control t writes, its reduction into the slot
@@ -431,12 +435,12 @@ int NewtonKrylov::device_steps() {
         return arn_reduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
                                      E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
       });
-    rc = E_.reduce_async(nw, nval, nval, slot);
-    return rc ? rc : control(t + 1);
+    rc = E_.reduce_async(nw, nval, nval, slot, false);
+    return rc ? rc : control(t + 1, true);
   };
   // one fused step queued beyond the one whose control is awaited, so the stream never waits
   // for the host; a step handed back leaves at most one launch pair behind that does nothing
-  int rc = control(t0);
+  int rc = control(t0, false);  // step t0's results came through the host's reduce_async
   int next = t0;  // the next fused step to queue
   if (!rc) rc = issue(next++);
   int t = t0;

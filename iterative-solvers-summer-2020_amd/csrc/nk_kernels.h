@@ -216,8 +216,10 @@ constexpr int kCtlPrm = kArnMaxNV + 4;
 // so the host needs no read-back when the device hands a step back.  status[t] (pinned host
 // memory) <- 1 (continued) or 2 (handed back) after those writes.  Nothing runs once S->halt is
 // set.
-hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* prm,
-                          uint32_t* status, int t, hipStream_t s);
+// red_host (optional, pinned): the kernel also copies `red` there (the host reads it when the
+// step is handed back; saves the all-reduce path its D2H copy per step).
+hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
+                          double* prm, uint32_t* status, int t, hipStream_t s);
 // The same preceded by the reduction of the fused step's partials (one GPU: no all-reduce in
 // between) in one launch: result[k] = sum_b partial[k nblk + b] for k < nval (and result_host,
 // pinned), then the last block to finish runs the control of step t on result.

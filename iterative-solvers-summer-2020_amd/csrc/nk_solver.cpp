@@ -232,7 +232,7 @@ uint32_t Engine::wait_flag(const uint32_t* flag) {
   return v;
 }
 
-int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot) {
+int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot, bool host_copy) {
   if (slot < 0 || slot + nv > kReduceSlots) return NK_EINVAL;
   // any communicator (also a world of one) takes the all-reduce path
   const bool multi = comm != nullptr;
@@ -247,7 +247,7 @@ int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot) {
   });
   if (rc || !multi) return rc;
   rc = comm->allreduce(dres_ + slot, nsum, nv, s);
-  if (rc) return rc;
+  if (rc || !host_copy) return rc;
   return hipMemcpyAsync(hres_ + slot, dres_ + slot, sizeof(double) * nv, hipMemcpyDeviceToHost,
                         s) == hipSuccess
              ? NK_OK

@@ -104,7 +104,9 @@ class Engine {
   int reduce(int64_t nblk, int nsum, int nv, double* out);
   // The same without synchronising: the result lands in device slot dres(slot) (ordered on the
   // stream, all-reduced across ranks) and, after the next sync(), in host slot hres(slot).
-  int reduce_async(int64_t nblk, int nsum, int nv, int slot);
+  // host_copy = false: with a communicator, leave out the D2H copy of the all-reduced result
+  // (a device-side consumer copies what the host needs itself).
+  int reduce_async(int64_t nblk, int nsum, int nv, int slot, bool host_copy = true);
   const double* dres(int slot) const { return dres_ + slot; }
   const double* hres(int slot) const { return hres_ + slot; }
   double* dres_mut(int slot) const { return dres_ + slot; }  // for a kernel that writes a slot
