@@ -229,6 +229,57 @@ def test_config4_4096_step():
     assert float(np.abs(out["1"] - out["0"]).max()) <= 1e-5 * scale
 
 
+def _residual_rows(U1, U0, h, r, k, g, chunk=2048):
+    """The oracle residual (sh_scipy_nk.py:47-49) of a periodic grid, evaluated in row blocks:
+    each block is padded with the two rows either side (periodic), so the periodic stencil of
+    the padded block is exact on its interior rows; returns max |F|."""
+    ny, nx = U1.shape
+    worst = 0.0
+    for a in range(0, ny, chunk):
+        b = min(ny, a + chunk)
+        rows = np.arange(a - 2, b + 2) % ny
+        u1, u0 = U1[rows], U0[rows]
+        F = sh_oracle.residual(u1.reshape(-1), u0.reshape(-1), b - a + 4, nx, h, r, k, g)
+        worst = max(worst, float(np.abs(F.reshape(b - a + 4, nx)[2:-2]).max()))
+    return worst
+
+
+@pytest.mark.timeout(600)
+def test_config5_16384_eight_slabs():
+    """BASELINE config 5's decomposition: a 16384^2 grid cut into 8 row slabs (the 8-GPU layout,
+    here 8 loopback slabs on one GPU, one host thread each; RCCL carries the same protocol), one
+    FD step from default_rng(2020) at scipy's default f_tol with the device-side Arnoldi control
+    the communicator path uses.  Every slab reports the same Newton count, and the gathered state
+    is a root of the oracle residual over the whole grid to the max-norm tolerance."""
+    import nkhip
+    N, P = 16384, 8
+    U0 = np.random.default_rng(2020).standard_normal((N, N))
+    comms = nkhip.loopback_comms(P)
+    out, stats = [None] * P, [None] * P
+
+    def run(p):
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            row0, ny = nkhip.slab_rows(N, p, P)
+            m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, comm=comms[p], ny_local=ny, stream=stream)
+            u = torch.as_tensor(U0[row0:row0 + ny], device="cuda")
+            out[p] = m.step(u).cpu().numpy()
+            stats[p] = dict(m.last_stats)
+            stream.synchronize()
+            m.close()
+            del u
+    try:
+        run_slabs(comms, run, timeout=500)
+    finally:
+        torch.cuda.empty_cache()
+    assert all(st["status"] == 0 for st in stats), stats
+    assert len({st["nit"] for st in stats}) == 1 and 2 <= stats[0]["nit"] <= 10, stats
+    assert stats[0]["n_device_steps"] > 0
+    U1 = np.concatenate(out, axis=0)
+    del out
+    assert _residual_rows(U1, U0, 0.625, 0.01, 0.2, 1.0) <= 1.01 * np.finfo(float).eps ** (1 / 3)
+
+
 def test_rccl_world1_matches_single_slab():
     """The RCCL communicator path on one GPU: ncclCommInitRank, the grouped halo send/recv (to
     itself, prev == next == 0) and the in-stream all-reduces, against the plain periodic slab."""
