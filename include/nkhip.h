@@ -143,6 +143,12 @@ int nk_sh_arnoldi_fused_edges(const double* const* V_dev, const double* const* E
                               int64_t ny, int64_t nx, double h, double r, double k, double g,
                               double zs, double sc, double* v_out_dev, double* w_out_dev,
                               double* Ev_out_dev, double* Ew_out_dev, double* dots, void* stream);
+/* Block-halo mailbox of the fused step (no reference counterpart: a property of this kernel's
+ * grid).  The blocks of a band publish u on their edge columns and read their neighbours' instead
+ * of recomputing the halo from every update entry; NKHIP_ARN_MBOX=0 turns it off, =2 makes every
+ * consumer recompute (the path a missing neighbour takes).  Counts the fused launches, process-
+ * wide, that ran with it (nx a multiple of the kernel's block width, >= 2 blocks per band). */
+int64_t nk_arnoldi_mbox_launches(void);
 
 /* ---------------- BLAS-1 (scipy get_blas_funcs dot/nrm2/axpy/scal in _gcrotmk.py:104-126) ------ */
 /* Scalar results are written to host memory; the call synchronises `stream`. */

@@ -29,6 +29,7 @@
 // DPP/permlane sums form c_i V_i per column.  Each band recomputes v on the two rows above and
 // below it (band halo).  Per-lane sums are wave-reduced once at the end and written as one
 // partial per wave (deterministic: a fixed wave -> rows mapping and a fixed order).
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 
@@ -177,6 +178,44 @@ __device__ __forceinline__ dv2 gld2(const double* a) {
   return *p;
 }
 
+// ------------------------------------------------------------------------------------------
+// Mailbox: block halos exchanged between the blocks of a band instead of recomputed.
+//
+// A block's stencil needs u = v on the two columns either side of it, and v there is a sum over
+// every update entry: recomputing it costs each block one packed halo load per row touching ~14
+// distinct lines (the block-halo cost measured in profiles/r02_arnoldi_ab.md: a variant with no
+// halo load ran 10 % faster).  But the neighbouring block of the same band computes exactly those
+// values one iteration away, and one launch is one resident round of blocks whose bands sit on
+// one XCD (the blockIdx mapping below), so it PUBLISHES them: per row, its lanes holding the
+// block's first / last column pair store {u, tag} records (16 B each, device-coherent stores),
+// and the consumer polls them one row later than it used to need them (the halo of row q only
+// enters the window rows that the stencil centre reaches one iteration after row q is pushed:
+// push stores the edge lanes' sums without it (adding -0.0, exact), fixup adds it, and since
+// a + b == b + a the result is bitwise what the packed path computes from the same values).
+// The tag (unique per launch) makes stale records from earlier launches invisible, so the
+// buffer is never cleared.  A neighbour that is not there in time -- not resident, another
+// XCD -- is waited for a bounded number of polls, after which the lane recomputes the pair
+// itself, in the producer's exact summation order (same result bits), and stops polling for
+// the rest of the launch: correctness never depends on co-residency.
+#ifndef ARN_MB_AUX
+#define ARN_MB_AUX 16
+#endif
+constexpr uint32_t kMBCoh = ARN_MB_AUX;  // cache policy of the record loads / stores (16: sc1)
+constexpr int kMBSpin = 2048;     // polls before a lane recomputes a missing halo pair itself
+__device__ __forceinline__ uint32_t mb_off(int64_t blk, int64_t T, int64_t t, int side, int comp) {
+  return uint32_t((((blk * T + t) * 4) + side * 2 + comp) * 16);
+}
+__device__ __forceinline__ bool mb_tag_ok(const u32x4& a, uint64_t tag) {
+  return a.z == uint32_t(tag) && a.w == uint32_t(tag >> 32);
+}
+__device__ __forceinline__ double mb_val(const u32x4& a) {
+  return __builtin_bit_cast(double, u32x2{a.x, a.y});
+}
+__device__ __forceinline__ u32x4 mb_rec(double v, uint64_t tag) {
+  const u32x2 b = __builtin_bit_cast(u32x2, v);
+  return u32x4{b.x, b.y, uint32_t(tag), uint32_t(tag >> 32)};
+}
+
 // lane i <- lane i-1 (wave_shr:1) and lane i <- lane i+1 (wave_shl:1); lanes 0 / 63 get 0
 __device__ __forceinline__ double dpp_up(double x) {
   const u32x2 b = __builtin_bit_cast(u32x2, x);
@@ -209,7 +248,7 @@ __device__ __forceinline__ double dpp_down(double x) {
 // sums each half's entries and adds the other half's sum (v_permlane32_swap); both halves then
 // hold v, y and w' of the wave's 64 columns, and each half takes the dot products of its own
 // entries (half 0 also w'.v, v.v, w'.w').
-template <int NV, bool EXT, int PF, bool NT>
+template <int NV, bool EXT, int PF, bool NT, bool MB>
 __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
   double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
@@ -258,19 +297,19 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
   dv2 (*lg)[NB + 1][64] = lag[wid];
 
+  auto src = [&](int e) -> const double* {
+    if (e < NV) return A.V[e];
+    if (e == NV) return A.w;
+    if (e == EX) return A.x0;
+    return EXT ? A.z : A.x0;
+  };
+  auto cof = [&](int e) -> double { return e < NV ? cst[e] : (e == NV ? a_tau : 0.0); };
   // per-lane source of load k (entry 2k + hf) and its update coefficient; the padding entry
   // (NE odd) repeats the other half's address with coefficient 0
   const double* ep[NI];
   double ecf[NI];
 #pragma unroll
   for (int k = 0; k < NI; ++k) {
-    auto src = [&](int e) -> const double* {
-      if (e < NV) return A.V[e];
-      if (e == NV) return A.w;
-      if (e == EX) return A.x0;
-      return EXT ? A.z : A.x0;
-    };
-    auto cof = [&](int e) -> double { return e < NV ? cst[e] : (e == NV ? a_tau : 0.0); };
     const int e0 = 2 * k, e1 = (2 * k + 1 < NE) ? 2 * k + 1 : 2 * k;
     ep[k] = hf ? src(e1) : src(e0);
     ecf[k] = hf ? (2 * k + 1 < NE ? cof(e1) : 0.0) : cof(e0);
@@ -328,6 +367,78 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     q = (q > r1 + 1) ? r1 + 1 : q;  // past the band halo: re-read its last row
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
+  // a neighbour slab's halo row (u taken from A.yh)
+  auto halo_row = [&](int64_t q) -> bool {
+    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
+    return slab && (qc < 0 || qc >= ny);
+  };
+
+  // mailbox (see "Mailbox" above): wave 0's lanes l == 0 hold the block's first column pair and
+  // need its left halo pair, wave WPB-1's lanes l == 31 its last pair and the right halo pair
+  constexpr int BW = WPB * kSW;
+  constexpr bool mb = MB && !EXT;  // a separate instantiation: the plain one has none of it
+  const int64_t mbT = A.RY + 8;             // records per block and side (rows pushed <= RY + 7)
+  const __amdgpu_buffer_rsrc_t rmb = rsrc(A.mb, mb ? A.mb_cap : 0);
+  const uint64_t tag = A.mb_tag;
+  const bool needL = mb && wid == 0 && l == 0, needR = mb && wid == WPB - 1 && l == 31;
+  const int64_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
+  const int nside = needL ? 1 : 0;  // my left halo = the left neighbour's right-edge records
+  const bool prod = mb && ((wid == 0 && lane == 0) || (wid == WPB - 1 && lane == 31));
+  const int pside = (wid == 0 && lane == 0) ? 0 : 1;
+  const int64_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;  // the halo pair's columns
+  // this lane stopped polling (a neighbour was not there in time; mb_recompute: test switch)
+  bool mb_dead = A.mb_recompute;
+  auto mb_need = [&](int64_t q) -> bool { return (needL || needR) && !halo_row(q); };
+  auto poll = [&](int64_t q, u32x4* a, u32x4* b) {  // issue the two record loads of row q
+    const bool on = mb_need(q) && !mb_dead;
+    const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+    *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
+    *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
+  };
+  // the producer's value of the halo pair, recomputed in its summation order (rare path)
+  // (a rolled loop with uniform entry indices: few registers beside the march's live state)
+  auto ent = [&](int e) -> const double* {
+    return e < NV ? A.V[e] : (e == NV ? A.w : ((e == EX || !EXT) ? A.x0 : A.z));
+  };
+  auto cfd = [&](int e) -> double { return e < NV ? arn_c(A, e) : (e == NV ? a_tau : 0.0); };
+  auto recompute = [&](int64_t q) -> dv2 {
+    const int64_t o2 = wrap(q) * nx + fcol;
+    double p0x = 0.0, p0y = 0.0, p1x = 0.0, p1y = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < NI; ++k) {
+      const bool two = 2 * k + 1 < NE;
+      const int e0 = 2 * k, e1 = two ? 2 * k + 1 : 2 * k;
+      const dv2 x = gld2<false>(ent(e0) + o2), y = gld2<false>(ent(e1) + o2);
+      const double c0 = cfd(e0), c1 = two ? cfd(e1) : 0.0;
+      p0x = __builtin_fma(c0, x.x, p0x);
+      p0y = __builtin_fma(c0, x.y, p0y);
+      p1x = __builtin_fma(c1, y.x, p1x);
+      p1y = __builtin_fma(c1, y.y, p1y);
+    }
+    return dv2{p0x + p1x, p0y + p1y};
+  };
+  // the halo pair of row q (-0.0 where the lane needs none: adding it changes nothing)
+  auto mb_halo = [&](int64_t q, u32x4 a, u32x4 b) -> dv2 {
+    const bool need = mb_need(q);
+    bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
+    dv2 h{mb_val(a), mb_val(b)};
+    if (!ok) {  // the neighbour is behind (or was not there): poll, then recompute
+      const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+      for (int n = 0; n < kMBSpin && !mb_dead && !ok; ++n) {
+        __builtin_amdgcn_s_sleep(2);
+        a = __builtin_amdgcn_raw_buffer_load_b128(rmb, o, 0, kMBCoh);
+        b = __builtin_amdgcn_raw_buffer_load_b128(rmb, o + 16, 0, kMBCoh);
+        ok = mb_tag_ok(a, tag) && mb_tag_ok(b, tag);
+      }
+      if (ok) {
+        h = dv2{mb_val(a), mb_val(b)};
+      } else {
+        mb_dead = true;
+        h = recompute(q);
+      }
+    }
+    return need ? h : dv2{-0.0, -0.0};
+  };
 
   struct Slot {
     dv2 e[NI];
@@ -339,7 +450,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const int64_t qq = wrap(q);
     const int64_t o = qq * nx + col;
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
-    const bool hrow = slab && (qc < 0 || qc >= ny);
+    const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
@@ -348,10 +459,13 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       s.e[k] = gld2<NT>(a);
     }
     const int64_t ho = qq * nx + hcol;
-    // block halo: from the entry's edge array (four rows per line) or from the vector itself
+    // block halo: from the entry's edge array (four rows per line) or from the vector itself;
+    // with the mailbox a load of one fixed line (keeps the row's load batch the same shape)
     const int64_t eo = ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh;
-    if constexpr (!EXT) s.hv = gld(useE ? hE + eo : hp + ho);
-    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
+    if constexpr (!EXT && !mb) s.hv = gld(useE ? hE + eo : hp + ho);
+    // z on the halo columns (EXT, lanes 4..); u of a slab halo row (A.yh, lanes 0-3); every
+    // other lane one fixed line
+    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : (mb ? yhb : hxp + ho));
     s.own = !hrow;
   };
   // entry e of this row for both halves (e is a compile-time index)
@@ -379,9 +493,9 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   auto push = [&](const Slot& s, int64_t q) {
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
-    for (int k = 0; k < NI; ++k) {
-      p0 += ecf[k] * s.e[k].x;
-      p1 += ecf[k] * s.e[k].y;
+    for (int k = 0; k < NI; ++k) {  // explicit FMAs: the mailbox's recompute() repeats them
+      p0 = __builtin_fma(ecf[k], s.e[k].x, p0);
+      p1 = __builtin_fma(ecf[k], s.e[k].y, p1);
     }
     const dv2 v{pair_sum(p0), pair_sum(p1)};
     // the stencil input u = v (or the augmentation vector z); on a slab's halo row the x0
@@ -398,7 +512,17 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     // block halo: this wave's share of c_i V_i on the four halo columns (sum over the 16 lanes
     // of each column), exchanged with u on the edge columns of every wave through LDS
     const int slot = int(q & 1);
-    if constexpr (!EXT) {
+    // mailbox: publish u on this block's first / last column pair
+    {
+      if constexpr (mb) {
+        const bool pq = prod && s.own;
+        const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
+        __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
+                                               kMBCoh);
+      }
+    }
+    if constexpr (!EXT && !mb) {
       // lane 4e + hh holds entry e (16 per instruction) of halo column hh: sum the four entries
       // of each 16-lane row (DPP row shifts), then the rows in pairs (permlane16/32 swaps);
       // lanes 12..15 end with the totals
@@ -428,10 +552,11 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    double hz = 0.0;
+    double hz = -0.0;  // mailbox: the halo pair is added by fixup() one iteration later
     if constexpr (EXT) {
       hz = __shfl(s.hx, hh + 4, 64);
-    } else {
+    } else if constexpr (!mb) {
+      hz = 0.0;
 #pragma unroll
       for (int w = 0; w < WPB; ++w) hz += hpart[slot][w][hh];  // fixed order: deterministic
     }
@@ -540,6 +665,14 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     h2w[1] = h2w[2];
     h2w[2] = h2;
   };
+  // mailbox: the halo pair h of a row enters the window rows that hold it (hq: its h1 = u[c-1]
+  // + u[c+1], h2q: its h2 = u[c-2] + u[c+2]); push() left -0.0 in its place, and a + b == b + a
+  auto fixup = [&](dv2& hq, dv2& h2q, const dv2& h) {
+    hq.x = hq.x + (needL ? h.y : -0.0);
+    hq.y = hq.y + (needR ? h.x : -0.0);
+    h2q.x = h2q.x + h.x;
+    h2q.y = h2q.y + h.y;
+  };
 
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
@@ -560,6 +693,15 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
       stash(P[0], gq, r0);
       push_h2(P[1], r0 + 1);
       stash(P[1], gq, r0 + 1);
+      {  // halo pairs of rows r0-1 (window slot 2) and r0 (slot 3)
+        if constexpr (mb) {
+          u32x4 a0, b0, a1, b1;
+          poll(r0 - 1, &a0, &b0);
+          poll(r0, &a1, &b1);
+          fixup(hw[2], h2w[0], mb_halo(r0 - 1, a0, b0));
+          fixup(hw[3], h2w[1], mb_halo(r0, a1, b1));
+        }
+      }
       // whole groups of RR rows with no branch inside the group (a branch would make the
       // compiler's wait-count analysis drain every load in flight): rows past the band end
       // are computed on clamped rows and masked out of the stores and sums
@@ -567,8 +709,12 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 #pragma unroll
         for (int k = 0; k < RR; ++k) {
           const int64_t r = r0 + t0 + k;
+          u32x4 ma, mb2;
+          if constexpr (mb) poll(r + 1, &ma, &mb2);  // before the row's batch: its wait
+                                                     // leaves the batch in flight
           load(S[(k + PF) % RR], r + 2 + PF);  // the slot of row r+1, consumed last step
           push_h2(S[k], r + 2);
+          if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(r + 1, ma, mb2));  // row r+1
           centre(r);
           stash(S[k], gq, r + 2);  // into the LDS slot row r just vacated
         }
@@ -619,7 +765,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
 constexpr int kWW = 128;       // columns per wave
 constexpr int kWideMaxNV = 18;  // LDS: 2 rows x (nv + 1) x 4 waves x 1 KB <= 152 KB
 
-template <int NV, bool EXT, int PF, bool NT, int W>
+template <int NV, bool EXT, int PF, bool NT, int W, bool MB>
 __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
   double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
@@ -705,6 +851,65 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     q = (q > r1 + 1) ? r1 + 1 : q;
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
+  auto halo_row = [&](int64_t q) -> bool {
+    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
+    return slab && (qc < 0 || qc >= ny);
+  };
+
+  // mailbox, as in arnoldi_kernel: wave 0's lane 0 holds the first column pair and needs the
+  // left halo pair, wave W-1's lane 63 the last pair and the right halo pair
+  constexpr int BW = W * kWW;
+  constexpr bool mb = MB && !EXT;
+  const int64_t mbT = A.RY + 8;
+  const __amdgpu_buffer_rsrc_t rmb = rsrc(A.mb, mb ? A.mb_cap : 0);
+  const uint64_t tag = A.mb_tag;
+  const bool needL = mb && wid == 0 && lane == 0, needR = mb && wid == W - 1 && lane == 63;
+  const int64_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
+  const int nside = needL ? 1 : 0;
+  const bool prod = needL || needR;
+  const int pside = needL ? 0 : 1;
+  const int64_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;
+  bool mb_dead = A.mb_recompute;
+  auto mb_need = [&](int64_t q) -> bool { return (needL || needR) && !halo_row(q); };
+  auto poll = [&](int64_t q, u32x4* a, u32x4* b) {
+    const bool on = mb_need(q) && !mb_dead;
+    const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+    *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
+    *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
+  };
+  auto recompute = [&](int64_t q) -> dv2 {  // push()'s update sum, entry order (rolled loop)
+    const int64_t o2 = wrap(q) * nx + fcol;
+    dv2 v{0.0, 0.0};
+#pragma unroll 1
+    for (int e = 0; e <= NV; ++e) {
+      const dv2 x = gld2<false>((e < NV ? A.V[e] : A.w) + o2);
+      const double cf = e < NV ? arn_c(A, e) : a_tau;
+      v.x = __builtin_fma(cf, x.x, v.x);
+      v.y = __builtin_fma(cf, x.y, v.y);
+    }
+    return v;
+  };
+  auto mb_halo = [&](int64_t q, u32x4 a, u32x4 b) -> dv2 {
+    const bool need = mb_need(q);
+    bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
+    dv2 h{mb_val(a), mb_val(b)};
+    if (!ok) {
+      const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+      for (int n = 0; n < kMBSpin && !mb_dead && !ok; ++n) {
+        __builtin_amdgcn_s_sleep(2);
+        a = __builtin_amdgcn_raw_buffer_load_b128(rmb, o, 0, kMBCoh);
+        b = __builtin_amdgcn_raw_buffer_load_b128(rmb, o + 16, 0, kMBCoh);
+        ok = mb_tag_ok(a, tag) && mb_tag_ok(b, tag);
+      }
+      if (ok) {
+        h = dv2{mb_val(a), mb_val(b)};
+      } else {
+        mb_dead = true;
+        h = recompute(q);
+      }
+    }
+    return need ? h : dv2{-0.0, -0.0};
+  };
 
   struct Slot {
     dv2 e[NE];
@@ -715,7 +920,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     const int64_t qq = wrap(q);
     const int64_t o = qq * nx + col;
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
-    const bool hrow = slab && (qc < 0 || qc >= ny);
+    const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
@@ -725,8 +930,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     const int64_t ho = qq * nx + hcol;
     const int64_t eo = ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh;
-    if constexpr (!EXT) s.hv = gld(useE ? hE + eo : hp + ho);
-    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : hxp + ho);
+    if constexpr (!EXT && !mb) s.hv = gld(useE ? hE + eo : hp + ho);
+    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : (mb ? yhb : hxp + ho));
     s.own = !hrow;
   };
   auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
@@ -744,8 +949,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     dv2 v{0.0, 0.0};
 #pragma unroll
     for (int e = 0; e <= NV; ++e) {  // entry order (the slab edge kernel sums the same way)
-      v.x += cof(e) * s.e[e].x;
-      v.y += cof(e) * s.e[e].y;
+      v.x = __builtin_fma(cof(e), s.e[e].x, v.x);
+      v.y = __builtin_fma(cof(e), s.e[e].y, v.y);
     }
     const dv2 xe = s.e[EX];
     gq = xe;
@@ -755,7 +960,16 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     else
       u = s.own ? v : xe;
     const int slot = int(q & 1);
-    if constexpr (!EXT) {
+    {  // mailbox: publish u on this block's first / last column pair
+      if constexpr (mb) {
+        const bool pq = prod && s.own;
+        const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
+        __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
+                                               kMBCoh);
+      }
+    }
+    if constexpr (!EXT && !mb) {
       double hs = hcf * s.hv;
       hs += dpp_row_shr(hs, 4);
       hs += dpp_row_shr(hs, 8);
@@ -774,10 +988,11 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    double hz = 0.0;
+    double hz = -0.0;  // mailbox: added by fixup()
     if constexpr (EXT) {
       hz = __shfl(s.hx, hh + 4, 64);
-    } else {
+    } else if constexpr (!mb) {
+      hz = 0.0;
 #pragma unroll
       for (int w = 0; w < W; ++w) hz += hpart[slot][w][hh];
     }
@@ -861,6 +1076,12 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     h2w[1] = h2w[2];
     h2w[2] = h2;
   };
+  auto fixup = [&](dv2& hq, dv2& h2q, const dv2& h) {  // as in arnoldi_kernel
+    hq.x = hq.x + (needL ? h.y : -0.0);
+    hq.y = hq.y + (needR ? h.x : -0.0);
+    h2q.x = h2q.x + h.x;
+    h2q.y = h2q.y + h.y;
+  };
 
   if (nrows > 0) {
     Slot P[2];
@@ -877,12 +1098,24 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     stash(P[0], gq, r0);
     push_h2(P[1], r0 + 1);
     stash(P[1], gq, r0 + 1);
+    {
+      if constexpr (mb) {
+        u32x4 a0, b0, a1, b1;
+        poll(r0 - 1, &a0, &b0);
+        poll(r0, &a1, &b1);
+        fixup(hw[2], h2w[0], mb_halo(r0 - 1, a0, b0));
+        fixup(hw[3], h2w[1], mb_halo(r0, a1, b1));
+      }
+    }
     for (int64_t t0 = 0; t0 < nrows; t0 += RR) {  // no branch inside a group (see arnoldi_kernel)
 #pragma unroll
       for (int k = 0; k < RR; ++k) {
         const int64_t r = r0 + t0 + k;
+        u32x4 ma, mb2;
+        if constexpr (mb) poll(r + 1, &ma, &mb2);
         load(S[(k + PF) % RR], r + 2 + PF);
         push_h2(S[k], r + 2);
+        if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(r + 1, ma, mb2));
         centre(r);
         stash(S[k], gq, r + 2);
       }
@@ -910,6 +1143,8 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? std::atoi(v) : dflt;
 }
 
+std::atomic<int64_t> g_mbox_launches{0};
+
 struct Occ {
   int ncu = 0, blocks_per_cu = 0;
 };
@@ -918,7 +1153,8 @@ struct Occ {
 // `nwb` waves of `cw` columns each; bands of >= 8 rows, and no more partial columns than the
 // caller's buffer holds.  `occ` = that kernel's occupancy.
 template <int NV, class K>
-hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, hipStream_t s,
+hipError_t launch_grid(K kern, const Occ& occ, K kern_mb, const Occ& occ_mb, bool has_mb, int nwb,
+                       int cw, ArnoldiArgs A, hipStream_t s,
                        int64_t* nwaves) {
   if (occ.ncu == 0) return hipErrorUnknown;
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
@@ -934,6 +1170,12 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, h
   if (nbands > cap_bands) nbands = cap_bands;
   if (nbands > rows / 8) nbands = rows / 8;
   if (nbands < 1) nbands = 1;
+  // the mailbox: whole periodic rows of >= 2 blocks; a multiple of 8 bands, so that each XCD's
+  // contiguous run of blocks (the blockIdx mapping in the kernels) holds whole bands
+  const int64_t ngr = (strips + nwb - 1) / nwb;
+  bool mbox = has_mb && A.mb && !A.z && A.nx % (int64_t(nwb) * cw) == 0 && ngr >= 2 && rb == 0 &&
+              re == A.ny && occ_mb.blocks_per_cu == occ.blocks_per_cu;
+  if (mbox && nbands >= 8) nbands -= nbands % 8;
   const int64_t RY = (rows + nbands - 1) / nbands;
   nbands = (rows + RY - 1) / RY;
   const int64_t nw = wpr * nbands;
@@ -948,6 +1190,13 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, int cw, ArnoldiArgs A, h
   A.strips = int(strips);
   A.nbands = int(nbands);
   A.RY = int(RY);
+  if (mbox && ngr * nbands * (RY + 8) * 8 > A.mb_cap) mbox = false;  // records for every block
+  if (mbox) {
+    kern = kern_mb;  // the mailbox instantiation
+    g_mbox_launches.fetch_add(1, std::memory_order_relaxed);
+  } else {
+    A.mb = nullptr;
+  }
   int64_t blocks = (nw + nwb - 1) / nwb;
   blocks = (blocks + 7) / 8 * 8;
   *nwaves = nw;
@@ -972,18 +1221,22 @@ Occ query_occ(K kern, int threads) {
 
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
-  auto kern = arnoldi_kernel<NV, EXT, PF, NT>;
+  auto kern = arnoldi_kernel<NV, EXT, PF, NT, false>;
+  auto kern_mb = arnoldi_kernel<NV, EXT, PF, NT, !EXT>;  // EXT: no mailbox, the same kernel
   if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
   static const Occ occ = query_occ(kern, 64 * WPB);
-  return launch_grid<NV>(kern, occ, WPB, kSW, A, s, nwaves);
+  static const Occ occ_mb = query_occ(kern_mb, 64 * WPB);
+  return launch_grid<NV>(kern, occ, kern_mb, occ_mb, !EXT, WPB, kSW, A, s, nwaves);
 }
 
 constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
-  auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW>;
+  // no mailbox instantiation: with 512-column blocks the packed halo is the cheaper one
+  // (4096^2, one box: n4 0.63 vs 0.55, n12 0.64 vs 0.63, n18 0.62 vs 0.57 of 8 TB/s)
+  auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW, false>;
   static const Occ occ = query_occ(kern, 64 * kWideW);
-  return launch_grid<NV>(kern, occ, kWideW, kWW, A, s, nwaves);
+  return launch_grid<NV>(kern, occ, kern, occ, false, kWideW, kWW, A, s, nwaves);
 }
 
 template <int NV, bool EXT>
@@ -1064,16 +1317,16 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           if (e + q < h0)
-            p0 += cof(e + q) * x[q];
+            p0 = __builtin_fma(cof(e + q), x[q], p0);
           else
-            p1 += cof(e + q) * x[q];
+            p1 = __builtin_fma(cof(e + q), x[q], p1);
         }
       }
       for (; e < ne; ++e) {
         if (e < h0)
-          p0 += cof(e) * ent(e)[o];
+          p0 = __builtin_fma(cof(e), ent(e)[o], p0);
         else
-          p1 += cof(e) * ent(e)[o];
+          p1 = __builtin_fma(cof(e), ent(e)[o], p1);
       }
     }
     for (; e + 8 <= ne; e += 8) {
@@ -1082,16 +1335,16 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
       for (int q = 0; q < 8; ++q) x[q] = ent(e + q)[o];
 #pragma unroll
       for (int q = 0; q < 8; q += 2) {
-        p0 += cof(e + q) * x[q];
-        p1 += cof(e + q + 1) * x[q + 1];
+        p0 = __builtin_fma(cof(e + q), x[q], p0);
+        p1 = __builtin_fma(cof(e + q + 1), x[q + 1], p1);
       }
     }
     for (; e < ne; ++e) {
       const double x = ent(e)[o];
       if (e & 1)
-        p1 += cof(e) * x;
+        p1 = __builtin_fma(cof(e), x, p1);
       else
-        p0 += cof(e) * x;
+        p0 = __builtin_fma(cof(e), x, p0);
     }
     y = p0 + p1;
   }
@@ -1136,6 +1389,13 @@ hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) 
   hipLaunchKernelGGL(arnoldi_edge_kernel, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256), 0, s,
                      A, y4, edge_split_point(A.nv));
   return hipGetLastError();
+}
+
+int64_t arnoldi_mbox_launches() { return g_mbox_launches.load(std::memory_order_relaxed); }
+
+int arnoldi_mbox_mode() {
+  const char* e = std::getenv("NKHIP_ARN_MBOX");
+  return (e && *e) ? std::atoi(e) : 1;
 }
 
 bool arnoldi_wide(int nv) {

@@ -153,6 +153,33 @@ int nk_sh_fdjvp(const double* x0, const double* G0, const double* z, double* y, 
 }
 
 namespace {
+// the mailbox of the kernel-level entry points (one buffer for every caller; a launch on another
+// stream that overwrites records only sends consumers to their recompute path)
+int attach_mbox(ArnoldiArgs& A) {
+  const int mode = arnoldi_mbox_mode();
+  if (mode == 0) return NK_OK;
+  static std::mutex mu;
+  static double* buf = nullptr;
+  static int64_t cap = 0;
+  static uint64_t tag = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  const int64_t need = arnoldi_mbox_elems(A.ny, A.nx);
+  if (cap < need) {
+    if (buf) hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), sizeof(double) * need) != hipSuccess)
+      return NK_ENOMEM;
+    if (hipMemset(buf, 0, sizeof(double) * need) != hipSuccess) return NK_EHIP;
+    cap = need;
+  }
+  A.mb = buf;
+  A.mb_cap = cap;
+  A.mb_tag = ++tag;
+  A.mb_recompute = mode == 2;
+  return NK_OK;
+}
+
 int arnoldi_fused_call(const double* const* V, const double* const* E, const double* coef,
                        int32_t nv, const double* w, double tau, const double* x0, const double* G0,
                        const double* z, int64_t ny, int64_t nx, double h, double r, double k,
@@ -188,6 +215,7 @@ int arnoldi_fused_call(const double* const* V, const double* const* E, const dou
   A.k = sh_coef(h, r, k, g);
   A.out_v = v_out;
   A.out_w = w_out;
+  if (int rc = attach_mbox(A)) return rc;
   const int nval = 2 * nv + 3;
   if (!dots) {  // no reduction wanted (timing): a persistent partial buffer, no synchronisation
     static std::mutex mu;  // the buffer is shared by every caller thread
@@ -216,6 +244,8 @@ int arnoldi_fused_call(const double* const* V, const double* const* E, const dou
                      });
 }
 }  // namespace
+
+int64_t nk_arnoldi_mbox_launches(void) { return arnoldi_mbox_launches(); }
 
 int nk_sh_arnoldi_fused(const double* const* V, const double* coef, int32_t nv, const double* w,
                         double tau, const double* x0, const double* G0, const double* z,

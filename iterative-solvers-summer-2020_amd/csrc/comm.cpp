@@ -124,6 +124,7 @@ struct LoopComm final : nk_comm {
   int r = 0;
   int rank() const override { return r; }
   int size() const override { return sh->p; }
+  bool shares_device() const override { return true; }
 
   int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
     std::vector<double> host(nv);

@@ -27,6 +27,9 @@ struct nk_comm {
   // thread) marks the group aborted: peers blocked in (or entering) a collective return
   // NK_ECOMM instead of waiting forever.  RCCL: ncclCommAbort.
   virtual void abort() = 0;
+  // the ranks' kernels share one device (loopback): launches of different ranks run
+  // concurrently, so a kernel cannot count on its whole grid being resident
+  virtual bool shares_device() const { return false; }
 };
 
 namespace nk {

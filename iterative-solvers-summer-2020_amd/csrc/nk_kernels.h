@@ -168,7 +168,23 @@ struct ArnoldiArgs {
   // ctl[kCtlPrm] the control kernel wrote instead of the fields above, and the launch does
   // nothing when its halt entry is set (the control handed the loop back to the host)
   const double* ctl = nullptr;
+  // block-halo mailbox (plain launches over whole periodic rows only; see arnoldi.hip "Mailbox"):
+  // the blocks of a band publish u on their two edge column pairs per row, tagged with mb_tag
+  // (unique per launch), and read their neighbours' instead of recomputing the halo from every
+  // update entry.  mb == nullptr, or a grid it does not fit: the packed halo loads.
+  double* mb = nullptr;
+  int64_t mb_cap = 0;  // doubles at mb
+  uint64_t mb_tag = 0;
+  bool mb_recompute = false;  // test switch: every halo pair takes the mailbox's recompute path
 };
+// doubles of mailbox a grid of ny rows and nx columns may need (any layout, any band count)
+inline int64_t arnoldi_mbox_elems(int64_t ny, int64_t nx) {
+  return (2 * ny + 64) * (nx / 128 + 2) * 8;
+}
+// NKHIP_ARN_MBOX (read per call): 0 = packed halo loads, 1 = mailbox (default), 2 = mailbox with
+// every halo pair recomputed by its consumer (the path a missing neighbour takes; tests)
+int arnoldi_mbox_mode();
+int64_t arnoldi_mbox_launches();  // fused launches that ran with the mailbox (process-wide)
 bool arnoldi_supported(int nv, int64_t ny, int64_t nx);
 // basis length nv runs the wide layout (128-column waves, 512-column blocks; NKHIP_ARN_WIDE=0: off)
 bool arnoldi_wide(int nv);

@@ -13,6 +13,19 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
     : E_(E), ny_(ny), nx_(nx), ny_g_(ny_global), c_(c), jvp_mode_(jvp_mode) {
   // edge arrays for the fused Arnoldi kernel's block halos (1/64 of each pool vector)
   if (arnoldi_supported(1, ny, nx)) E_.enable_edges(ny, nx);
+  // the fused kernel's mailbox, unless the slabs of several ranks share this device (their
+  // launches run concurrently, so a band's blocks need not be resident together)
+  if (arnoldi_supported(1, ny, nx) && !(E_.comm && E_.comm->shares_device())) {
+    const int64_t n = arnoldi_mbox_elems(ny, nx);
+    if (hipMalloc(reinterpret_cast<void**>(&mb_), sizeof(double) * n) == hipSuccess &&
+        hipMemset(mb_, 0, sizeof(double) * n) == hipSuccess) {
+      mb_cap_ = n;
+    } else {
+      if (mb_) hipFree(mb_);
+      mb_ = nullptr;  // optional: the packed halo loads
+      (void)hipGetLastError();
+    }
+  }
   if (hipMalloc(reinterpret_cast<void**>(&B_), sizeof(double) * Engine::pad(ny * nx)) !=
       hipSuccess) {
     B_ = nullptr;
@@ -60,6 +73,7 @@ SHProblem::~SHProblem() {
   if (side_) hipStreamSynchronize(side_);
   if (B_) hipFree(B_);
   if (hx_) hipFree(hx_);
+  if (mb_) hipFree(mb_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
   if (side_) hipStreamDestroy(side_);
@@ -261,6 +275,15 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     for (int i = 0; i <= nv; ++i) A.E[i] = nullptr;
   A.Eout_v = E_.edges(out_v);
   A.Eout_w = E_.edges(out_w);
+  if (mb_) {
+    const int mode = arnoldi_mbox_mode();
+    if (mode != 0) {
+      A.mb = mb_;
+      A.mb_cap = mb_cap_;
+      A.mb_tag = ++mb_tag_;
+      A.mb_recompute = mode == 2;
+    }
+  }
   // algorithmic bytes per row: read V (nv), w, x0 (, z); write v, w'
   const double rowb = 8.0 * double(nx_) * (nv + 4 + (z ? 1 : 0));
   if (!dist())

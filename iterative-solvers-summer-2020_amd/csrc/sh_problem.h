@@ -54,6 +54,9 @@ class SHProblem final : public Problem {
   int64_t ny_min_ = 0, ny_max_ = 0;  // smallest / largest slab over the ranks
   hipStream_t side_ = nullptr;       // interior rows of the JVP while the halo is in flight
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  double* mb_ = nullptr;  // the fused kernel's block-halo mailbox (arnoldi.hip)
+  int64_t mb_cap_ = 0;
+  uint64_t mb_tag_ = 0;   // one tag per fused launch
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):

@@ -84,6 +84,7 @@ SIGNATURES = [
                                       _I64, _I64, _D, _D, _D, _D, _D, _D, _P, _P,
                                       C.POINTER(_D), _P]),
     ("nk_edge_elems", C.c_int64, [_I64, _I64]),
+    ("nk_arnoldi_mbox_launches", C.c_int64, []),
     ("nk_edge_gather", C.c_int, [_P, _P, _I64, _I64, _P]),
     ("nk_sh_arnoldi_fused_edges", C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_D), _I32,
                                             _P, _D, _P, _P, _P, _I64, _I64, _D, _D, _D, _D, _D,

@@ -132,6 +132,12 @@ def sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc, z=None, ny=Non
     return v_out, w_out, (list(dots) if reduce else None)
 
 
+def arnoldi_mbox_launches() -> int:
+    """Fused Arnoldi launches (process-wide) whose block halos went through the mailbox
+    (csrc/arnoldi.hip "Mailbox"; NKHIP_ARN_MBOX=0 turns it off)."""
+    return int(lib.nk_arnoldi_mbox_launches())
+
+
 def edge_gather(v, ny=None, nx=None, out=None):
     """The edge array of grid vector v (nkhip.h, nk_edge_gather): the two columns either side of
     every 256-column group boundary, four values per boundary and row."""

@@ -240,3 +240,94 @@ def test_device_control_default_tolerance():
     assert abs(sa[0]["nit"] - sb[0]["nit"]) <= 1 and sb[0]["n_device_steps"] > 0
     F = sh_oracle.residual(b.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
     assert np.abs(F).max() <= 1.01 * np.finfo(float).eps ** (1 / 3)
+
+
+def _mbox_expected(nv, nx):
+    """Whether the fused kernel's grid takes the mailbox: the vector-pair layout (nv >= 19;
+    the wide layout keeps its packed halo loads) with nx a multiple of its 256-column blocks and
+    two blocks per band at least."""
+    return nv >= 19 and nx % 256 == 0 and nx // 256 >= 2
+
+
+@pytest.mark.parametrize("ny,nx", [(64, 1024), (40, 512), (24, 2048)])
+@pytest.mark.parametrize("nv", [1, 6, 18, 19, 27, 35])
+def test_fused_kernel_mailbox(ny, nx, nv, monkeypatch):
+    """Block halos through the mailbox (arnoldi.hip "Mailbox": the blocks of a band publish u on
+    their edge columns): bitwise the same v, w' and dots as every consumer recomputing its halo
+    pair itself (NKHIP_ARN_MBOX=2, the path a missing neighbour takes); v bitwise and w', dots
+    within rounding of the packed halo loads (NKHIP_ARN_MBOX=0, which sum the halo in another
+    order); the mailbox ran exactly where the grid allows it."""
+    import nkhip
+    gen = torch.Generator(device="cpu").manual_seed(nv * 7 + nx + ny)
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    V = [rnd() for _ in range(nv)]
+    coef = [float(c) for c in torch.randn(nv, generator=gen, dtype=torch.float64)]
+    w, x0 = rnd(), rnd()
+    args = (V, coef, w, 0.75, x0, None, 0.625, 0.01, 0.2, 1.0, 0.5, 1e-3)
+    res, used = {}, {}
+    for mode in ("1", "2", "0"):
+        monkeypatch.setenv("NKHIP_ARN_MBOX", mode)
+        n0 = nkhip.arnoldi_mbox_launches()
+        res[mode] = nkhip.sh_arnoldi_fused(*args)
+        used[mode] = nkhip.arnoldi_mbox_launches() - n0
+    on = _mbox_expected(nv, nx)
+    assert used == {"1": int(on), "2": int(on), "0": 0}, used
+    (v1, w1, d1), (v2, w2, d2), (v0, w0, d0) = res["1"], res["2"], res["0"]
+    assert torch.equal(v1, v2) and torch.equal(w1, w2) and d1 == d2
+    assert torch.equal(v1, v0)
+    assert float((w1 - w0).abs().max()) <= 1e-12 * float(w0.abs().max())
+    scale = float(w0.norm()) * float(max(t.norm() for t in V + [v0])) + float(v0.norm()) ** 2
+    assert max(abs(a - b) for a, b in zip(d1, d0)) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("ny,nx", [(128, 1024), (64, 512)])
+def test_mailbox_solve(ny, nx, monkeypatch):
+    """The solver with the mailbox (default) is bitwise the solver whose consumers all recompute
+    their halo pairs (NKHIP_ARN_MBOX=2), and reaches the root of the packed-halo solver
+    (NKHIP_ARN_MBOX=0) to 1e-8 of the state's scale; the mailbox ran."""
+    import nkhip
+    n0 = nkhip.arnoldi_mbox_launches()
+    U0, a, sa, pa = _step(ny, nx, fused=True)
+    assert nkhip.arnoldi_mbox_launches() - n0 >= 1  # the vector-pair layout's (nv >= 19)
+    monkeypatch.setenv("NKHIP_ARN_MBOX", "2")
+    _, b, sb, _ = _step(ny, nx, fused=True)
+    monkeypatch.setenv("NKHIP_ARN_MBOX", "0")
+    n1 = nkhip.arnoldi_mbox_launches()
+    _, c, sc_, _ = _step(ny, nx, fused=True)
+    assert nkhip.arnoldi_mbox_launches() == n1
+    assert np.array_equal(a, b) and sa == sb
+    assert np.abs(a - c).max() <= 1e-8 * max(1.0, np.abs(c).max())
+    assert abs(sa[0]["nit"] - sc_[0]["nit"]) <= 1
+    F = sh_oracle.residual(a.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
+    assert np.abs(F).max() <= 1e-9
+
+
+def test_fused_kernel_mailbox_every_length(monkeypatch):
+    """Every basis length 1..35 (one kernel instantiation each; the mailbox from 19 on) at 32x1024:
+    bitwise the recompute path's v, w' and dots, and v, w' within rounding of an fp64 torch
+    reference (sh_scipy_nk.py:47-49 residual, _nonlin.py:1505-1513 quotient)."""
+    import nkhip
+    ny, nx = 32, 1024
+    h, r, k, g, tau, zs, sc = 0.625, 0.01, 0.2, 1.0, 0.75, 0.5, 1e-3
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    Vall = [rnd() for _ in range(35)]
+    w, x0 = rnd(), rnd()
+    G0 = _torch_G(x0, h, r, k, g)
+    for nv in range(1, 36):
+        print("nv", nv, flush=True)
+        V = Vall[:nv]
+        coef = [0.3 / nv * (1 + (i % 3)) for i in range(nv)]
+        n0 = nkhip.arnoldi_mbox_launches()
+        monkeypatch.setenv("NKHIP_ARN_MBOX", "1")
+        v1, w1, d1 = nkhip.sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc)
+        monkeypatch.setenv("NKHIP_ARN_MBOX", "2")
+        v2, w2, d2 = nkhip.sh_arnoldi_fused(V, coef, w, tau, x0, G0, h, r, k, g, zs, sc)
+        assert nkhip.arnoldi_mbox_launches() - n0 == (2 if nv >= 19 else 0), nv
+        assert torch.equal(v1, v2) and torch.equal(w1, w2) and d1 == d2, nv
+        vr = tau * w
+        for c, Vi in zip(coef, V):
+            vr = vr + c * Vi
+        wr = (_torch_G(x0 + sc * zs * vr, h, r, k, g) - G0) / sc
+        assert float((v1 - vr).abs().max()) <= 1e-13 * float(vr.abs().max()), nv
+        assert float((w1 - wr).abs().max()) <= 1e-9 * float(wr.abs().max()), nv
