@@ -1289,6 +1289,7 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
 // 4, .. of [V_0 .. V_{nv-1}, w] in one partial, 1, 3, 5, .. in the other, then their sum; for the
 // wide layout (h0 = nv + 1) all entries in order -- so a halo row
 // equals the row its owner computes.
+template <int NV>
 __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4,
                                                            int h0) {
   const double a_tau = arn_tau(A);
@@ -1302,53 +1303,40 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
   if (A.z) {
     y = A.z[o];
   } else {
-    // entries [V_0 .. V_{nv-1}, w] in batches of 8 loads in flight (the kernel is latency-bound:
-    // 4 rows of a slab); the sums stay in entry order within each parity
-    const int ne = A.nv + 1;
-    auto ent = [&](int e) -> const double* { return (e < A.nv) ? A.V[e] : A.w; };
-    auto cof = [&](int e) -> double { return (e < A.nv) ? arn_c(A, e) : a_tau; };
+    // every entry of [V_0 .. V_{nv-1}, w] and its coefficient in flight at once (the kernel is
+    // latency-bound: 4 rows of a slab -- batches of 8 took 10 us per launch); the sums then run
+    // in entry order within each partial
+    constexpr int NE = NV + 1;
+    double x[NE], cf[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      x[e] = ((e < NV) ? A.V[e] : A.w)[o];
+      cf[e] = (e < NV) ? arn_c(A, e) : a_tau;
+    }
     double p0 = 0.0, p1 = 0.0;
-    int e = 0;
-    if (h0 > 0) {  // entries [0, h0) in order, then [h0, ne) (wide layout: h0 = ne)
-      for (; e + 8 <= ne; e += 8) {
-        double x[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) x[q] = ent(e + q)[o];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if (e + q < h0)
-            p0 = __builtin_fma(cof(e + q), x[q], p0);
-          else
-            p1 = __builtin_fma(cof(e + q), x[q], p1);
-        }
-      }
-      for (; e < ne; ++e) {
-        if (e < h0)
-          p0 = __builtin_fma(cof(e), ent(e)[o], p0);
-        else
-          p1 = __builtin_fma(cof(e), ent(e)[o], p1);
-      }
-    }
-    for (; e + 8 <= ne; e += 8) {
-      double x[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) x[q] = ent(e + q)[o];
-#pragma unroll
-      for (int q = 0; q < 8; q += 2) {
-        p0 = __builtin_fma(cof(e + q), x[q], p0);
-        p1 = __builtin_fma(cof(e + q + 1), x[q + 1], p1);
-      }
-    }
-    for (; e < ne; ++e) {
-      const double x = ent(e)[o];
-      if (e & 1)
-        p1 = __builtin_fma(cof(e), x, p1);
+    for (int e = 0; e < NE; ++e) {
+      // wide layout (h0 = nv + 1): all in p0; vector pairs (h0 = 0): even entries in p0
+      if ((h0 > 0) ? (e < h0) : ((e & 1) == 0))
+        p0 = __builtin_fma(cf[e], x[e], p0);
       else
-        p0 = __builtin_fma(cof(e), x, p0);
+        p1 = __builtin_fma(cf[e], x[e], p1);
     }
     y = p0 + p1;
   }
   y4[int64_t(t) * A.nx + j] = y;
+}
+
+template <int NV = 1>
+hipError_t edge_launch_nv(const ArnoldiArgs& A, double* y4, int h0, hipStream_t s) {
+  if constexpr (NV > kArnMaxNV) {
+    return hipErrorInvalidValue;
+  } else {
+    if (A.nv != NV) return edge_launch_nv<NV + 1>(A, y4, h0, s);
+    hipLaunchKernelGGL(arnoldi_edge_kernel<NV>, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256),
+                       0, s, A, y4, h0);
+    return hipGetLastError();
+  }
 }
 
 // E[(b ny + q) 4 + 0..3] = v[q][B-2], v[q][B-1], v[q][B], v[q][B+1], B = kEdgeW b, columns mod nx
@@ -1386,9 +1374,7 @@ int edge_split_point(int nv) {
 
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) {
   if (A.ny < 4 || A.nx < 1 || !y4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(arnoldi_edge_kernel, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256), 0, s,
-                     A, y4, edge_split_point(A.nv));
-  return hipGetLastError();
+  return edge_launch_nv(A, y4, edge_split_point(A.nv), s);
 }
 
 int64_t arnoldi_mbox_launches() { return g_mbox_launches.load(std::memory_order_relaxed); }

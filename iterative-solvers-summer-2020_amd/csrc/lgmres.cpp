@@ -457,11 +457,16 @@ int NewtonKrylov::device_steps() {
     if (next == t && next + 1 <= nvmax) rc = issue(next++);
   }
   // step t was handed back: the fused steps queued from t on do nothing; undo their rotations
+  int voided = 0;
   for (int u = next - 1; u >= t; --u) {
     if (!rot[u].fused) continue;
     Sv_ = rot[u].spare;
     V_[u + 1] = rot[u].v;
+    ++voided;
   }
+  // ... and their launches are no work in the kernel profile (the slab edge kernel is one too)
+  E_.void_last(K_ARNOLDI, voided);
+  if (E_.comm) E_.void_last(K_ARN_EDGE, voided);
   if (rc) return rc;
   if (S.j != t || S.halt != 1 + t) return NK_EHIP;
   S.halt = 0;

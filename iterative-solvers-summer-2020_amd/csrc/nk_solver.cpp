@@ -171,6 +171,23 @@ void Engine::harvest() {
   pend_.clear();
 }
 
+void Engine::void_last(int kind, int count) {
+  if (kind < 0 || kind >= K_NKINDS) return;
+  for (int c = 0; c < count && c < kRecent && stats_[kind].launches > 0; ++c) {
+    const int64_t idx = stats_[kind].launches - 1;
+    stats_[kind].launches = idx;
+    stats_[kind].bytes -= recent_bytes_[kind][idx % kRecent];
+    for (size_t i = 0; i < pend_.size(); ++i) {
+      if (pend_[i].kind == kind && pend_[i].idx == idx) {
+        free_ev_.push_back(pend_[i].a);
+        free_ev_.push_back(pend_[i].b);
+        pend_.erase(pend_.begin() + i);
+        break;
+      }
+    }
+  }
+}
+
 void Engine::reset_stats() {
   for (auto& k : stats_) k = KStat{};
   for (auto& t : tick_) t = 0;

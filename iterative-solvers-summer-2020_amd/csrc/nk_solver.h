@@ -127,6 +127,11 @@ class Engine {
   // stream synchronisation found it still unset (the writer did not run).
   uint32_t wait_flag(const uint32_t* flag);
   int copy(double* dst, const double* src, int64_t n);
+  // The last `count` launches of `kind` did nothing (device-controlled steps queued past a step
+  // the control handed back, nk_kernels.h arn_halted): take them out of the launch counts, the
+  // algorithmic bytes and, where they were timed, the timed sample -- a no-op timed with a fused
+  // step's bytes would inflate the roofline figure.
+  void void_last(int kind, int count);
 
   double* partial() const { return partial_; }
   int64_t partial_cap() const { return partial_cap_; }
@@ -158,7 +163,10 @@ class Engine {
     int kind;
     hipEvent_t a, b;
     double bytes;
+    int64_t idx;  // the launch's index in its class
   };
+  static constexpr int kRecent = 8;
+  double recent_bytes_[K_NKINDS][kRecent] = {};  // bytes of the latest launches per class
   std::vector<Pending> pend_;
   std::vector<hipEvent_t> free_ev_;
   KStat stats_[K_NKINDS];
@@ -177,8 +185,9 @@ int Engine::launch_on(int kind, double bytes, hipStream_t st, L&& fn) {
   if (timed) {
     b = ev();
     hipEventRecord(b, st);
-    pend_.push_back(Pending{kind, a, b, bytes});
+    pend_.push_back(Pending{kind, a, b, bytes, stats_[kind].launches});
   }
+  recent_bytes_[kind][stats_[kind].launches % kRecent] = bytes;
   stats_[kind].launches += 1;
   stats_[kind].bytes += bytes;
   log_launch(kind, bytes);

@@ -299,6 +299,35 @@ def test_rccl_world1_matches_single_slab():
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_rccl_world1_mailbox(overlap, monkeypatch):
+    """A slab of the multi-GPU path with the fused kernel's block-halo mailbox (a grid whose
+    vector-pair launches take it): the slab's halo rows come from the RCCL exchange, its column
+    halos through the mailbox, the Arnoldi control runs on the device.  Same root as the single
+    periodic slab; the mailbox ran (the split interior/edge launches of NKHIP_SLAB_OVERLAP=1 do
+    without it)."""
+    import nkhip
+    monkeypatch.setenv("NKHIP_SLAB_OVERLAP", overlap)
+    ny, nx = 128, 1024
+    U0 = np.random.default_rng(5).standard_normal((ny, nx))
+    single = nkhip.SwiftHohenberg(N=nx, ny=ny, d=0.625 * nx, f_tol=1e-10)
+    ref = single.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+    single.close()
+    comm = nkhip.RcclComm.create(nkhip.RcclComm.unique_id(), 0, 1)
+    try:
+        m = nkhip.SwiftHohenberg(N=nx, ny=ny, d=0.625 * nx, f_tol=1e-10, comm=comm, ny_local=ny)
+        n0 = nkhip.arnoldi_mbox_launches()
+        got = m.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+        used = nkhip.arnoldi_mbox_launches() - n0
+        st = dict(m.last_stats)
+        m.close()
+    finally:
+        comm.close()
+    assert (used > 0) == (overlap == "0"), used
+    assert st["n_device_steps"] > 0
+    assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
+
+
 def test_rccl_from_torch_distributed_world1():
     """bench.py's multi-GPU bring-up (nccl process group, unique id broadcast) at world size 1."""
     import os
