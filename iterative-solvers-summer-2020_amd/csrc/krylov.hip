@@ -66,6 +66,12 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   const int nv = 2 * np + 1;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  // small vectors (few chunks): blockIdx.y splits the basis into runs of vpy vectors, so the
+  // runs stream in parallel instead of one after another (each value's partial is summed in the
+  // same order either way)
+  const int vpy = (np + gridDim.y - 1) / gridDim.y;
+  const int vlo = min(np, int(blockIdx.y) * ((vpy + 3) / 4 * 4));
+  const int vhi = min(np, vlo + (vpy + 3) / 4 * 4);
   for (int t = lane; t < nv; t += 64) accw[wid][t] = 0.0;  // each wave zeroes its own slice
   double aa = 0.0;
   // rev: the blocks dispatched first take the last chunk groups; a group's chunks, their order and
@@ -82,13 +88,13 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
       gv[k] = g ? ld2<VEC>(g, base + k * 2 * BS, n) : make_double2(0.0, 0.0);
       aa += av[k].x * av[k].x + av[k].y * av[k].y;
     }
-    for (int i0 = 0; i0 < np; i0 += 4) {
+    for (int i0 = vlo; i0 < vhi; i0 += 4) {
       double s[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s[u] = 0.0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (i0 + u < np) {
+        if (i0 + u < vhi) {
           const double* p = P.p[i0 + u];
           double2 pv[PAIRS];
           if (p == g) {  // the Gram-row vector is already in registers: no second read
@@ -111,7 +117,7 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
       if (lane == 0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          if (i0 + u < np) {
+          if (i0 + u < vhi) {
             accw[wid][i0 + u] += s[u];
             accw[wid][np + i0 + u] += s[4 + u];
           }
@@ -124,6 +130,8 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   if (lane == 0) accw[wid][2 * np] += t[0];
   __syncthreads();
   for (int k = threadIdx.x; k < nv; k += BS) {
+    const int kv = (k < np) ? k : ((k < 2 * np) ? k - np : -1);  // vector of value k (-1: |a|^2)
+    if (kv >= 0 ? (kv < vlo || kv >= vhi) : blockIdx.y != 0) continue;  // another run's value
     double v = accw[0][k];
 #pragma unroll
     for (int w = 1; w < BS / 64; ++w) v += accw[w][k];
@@ -131,7 +139,9 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
   }
 }
 
-template <bool VEC, bool NT>
+// UNR: basis vectors whose loads are in flight together (2 at 4096^2, where the stream is
+// bandwidth-bound; 8 for small vectors, where each batch is one memory latency)
+template <bool VEC, bool NT, int UNR>
 __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
                                                    VecList P, int np, int64_t n, int cpb,
                                                    double* partial, bool rev) {
@@ -153,8 +163,25 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
         acc[k] = make_double2(0.0, 0.0);
       }
     }
-#pragma unroll 2
-    for (int i = 0; i < np; ++i) {
+    int i = 0;
+    for (; i + UNR <= np; i += UNR) {  // the sums stay in vector order
+      double2 pv[UNR][PAIRS];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+#pragma unroll
+        for (int k = 0; k < PAIRS; ++k) pv[u][k] = ld2s<VEC, NT>(P.p[i + u], base + k * 2 * BS, n);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const double c = P.c[i + u];
+#pragma unroll
+        for (int k = 0; k < PAIRS; ++k) {
+          acc[k].x += c * pv[u][k].x;
+          acc[k].y += c * pv[u][k].y;
+        }
+      }
+    }
+    for (; i < np; ++i) {
       const double* p = P.p[i];
       const double c = P.c[i];
       double2 pv[PAIRS];
@@ -254,6 +281,10 @@ __global__ void __launch_bounds__(256) shlin_diag_kernel(const double* U, const 
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// vectors of at most this many 2048-element chunks take the latency-bound variants (the
+// moving-mesh problems' 5551 / 2601 points; the SH grids have thousands of chunks)
+constexpr int64_t kSmallChunks = 32;
+
 }  // namespace
 
 static int env_int(const char* name, int dflt) {
@@ -289,15 +320,18 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
   const bool rev = traversal_reverse();
   static const bool nt = env_int("NKHIP_NT", 1) != 0;
+  // small vectors (the moving-mesh problems: 5551 points = 3 chunks): one block row per run of
+  // four basis vectors; the 4096^2 grid keeps one row
+  const dim3 grid(unsigned(nb), nb <= kSmallChunks ? unsigned((np + 3) / 4 > 0 ? (np + 3) / 4 : 1) : 1u);
   if (vec && nt)
-    hipLaunchKernelGGL((mdot_kernel<true, true>), dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P, np,
-                       n, cpb, partial, rev);
+    hipLaunchKernelGGL((mdot_kernel<true, true>), grid, dim3(BS), 0, s, a, g, P, np, n, cpb,
+                       partial, rev);
   else if (vec)
-    hipLaunchKernelGGL((mdot_kernel<true, false>), dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P,
-                       np, n, cpb, partial, rev);
+    hipLaunchKernelGGL((mdot_kernel<true, false>), grid, dim3(BS), 0, s, a, g, P, np, n, cpb,
+                       partial, rev);
   else
-    hipLaunchKernelGGL((mdot_kernel<false, false>), dim3(unsigned(nb)), dim3(BS), 0, s, a, g, P,
-                       np, n, cpb, partial, rev);
+    hipLaunchKernelGGL((mdot_kernel<false, false>), grid, dim3(BS), 0, s, a, g, P, np, n, cpb,
+                       partial, rev);
   return hipGetLastError();
 }
 
@@ -313,15 +347,24 @@ hipError_t combo_launch(double* out, const double* in, double cin, const VecList
   for (int i = 0; i < np; ++i) vec = vec && al16(P.p[i]);
   const bool rev = traversal_reverse();
   static const bool nt = env_int("NKHIP_NT", 1) != 0;
-  if (vec && nt)
-    hipLaunchKernelGGL((combo_kernel<true, true>), dim3(unsigned(nb)), dim3(BS), 0, s, out, in,
-                       cin, P, np, n, cpb, partial, rev);
-  else if (vec)
-    hipLaunchKernelGGL((combo_kernel<true, false>), dim3(unsigned(nb)), dim3(BS), 0, s, out, in,
-                       cin, P, np, n, cpb, partial, rev);
-  else
-    hipLaunchKernelGGL((combo_kernel<false, false>), dim3(unsigned(nb)), dim3(BS), 0, s, out, in,
-                       cin, P, np, n, cpb, partial, rev);
+  const dim3 grid{unsigned(nb)}, block{unsigned(BS)};
+  if (nb <= kSmallChunks) {  // small vectors: 8 basis vectors' loads in flight per batch
+    if (vec)
+      hipLaunchKernelGGL((combo_kernel<true, false, 8>), grid, block, 0, s, out, in, cin, P, np, n,
+                         cpb, partial, rev);
+    else
+      hipLaunchKernelGGL((combo_kernel<false, false, 8>), grid, block, 0, s, out, in, cin, P, np,
+                         n, cpb, partial, rev);
+  } else if (vec && nt) {
+    hipLaunchKernelGGL((combo_kernel<true, true, 2>), grid, block, 0, s, out, in, cin, P, np, n,
+                       cpb, partial, rev);
+  } else if (vec) {
+    hipLaunchKernelGGL((combo_kernel<true, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
+                       cpb, partial, rev);
+  } else {
+    hipLaunchKernelGGL((combo_kernel<false, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
+                       cpb, partial, rev);
+  }
   return hipGetLastError();
 }
 

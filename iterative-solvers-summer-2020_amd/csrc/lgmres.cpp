@@ -464,9 +464,8 @@ int NewtonKrylov::device_steps() {
     V_[u + 1] = rot[u].v;
     ++voided;
   }
-  // ... and their launches are no work in the kernel profile (the slab edge kernel is one too)
-  E_.void_last(K_ARNOLDI, voided);
-  if (E_.comm) E_.void_last(K_ARN_EDGE, voided);
+  // ... and their launches did no work: out of the kernel profile
+  P_.void_fused_steps(voided);
   if (rc) return rc;
   if (S.j != t || S.halt != 1 + t) return NK_EHIP;
   S.halt = 0;

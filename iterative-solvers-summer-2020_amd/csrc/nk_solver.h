@@ -230,6 +230,9 @@ struct Problem {
   // come from the device parameter block ctl, and the step does nothing when its halt entry is set.
   // v (a pool vector) may enter the update of a later fused step: refresh its edge array
   virtual int publish_edges(const double* /*v*/) { return NK_OK; }
+  // The last `count` fused steps were no-ops (queued past a step the device control handed
+  // back): take their launches out of the kernel profile (Engine::void_last).
+  virtual void void_fused_steps(int /*count*/) {}
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
 };

@@ -301,6 +301,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   // per Arnoldi step); the default is one launch after the exchange.
   const char* ov = std::getenv("NKHIP_SLAB_OVERLAP");
   const bool split = ny_ >= 12 && side_ && (ov && ov[0] == '1');
+  last_split_ = split;
   ArnoldiArgs I = A, T = A, Bm = A;
   int64_t nwI = 0, nwT = 0, nwB = 0;
   if (split) {
@@ -357,6 +358,12 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   });
   *nwaves = nwI + nwT + nwB;
   return rc;
+}
+
+void SHProblem::void_fused_steps(int count) {
+  E_.void_last(K_ARNOLDI, count);
+  if (dist()) E_.void_last(K_ARN_EDGE, count);  // the halo exchange still moves its rows
+  if (last_split_) E_.void_last(K_ARN_SLAB, count);
 }
 
 int SHProblem::publish_edges(const double* v) {

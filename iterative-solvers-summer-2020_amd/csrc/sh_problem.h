@@ -31,6 +31,7 @@ class SHProblem final : public Problem {
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
   int publish_edges(const double* v) override;
+  void void_fused_steps(int count) override;
 
  private:
   // any communicator (also a world of one: its halo is the periodic wrap through RCCL)
@@ -57,6 +58,7 @@ class SHProblem final : public Problem {
   double* mb_ = nullptr;  // the fused kernel's block-halo mailbox (arnoldi.hip)
   int64_t mb_cap_ = 0;
   uint64_t mb_tag_ = 0;   // one tag per fused launch
+  bool last_split_ = false;  // the last fused step ran as interior + edge-band launches
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):
