@@ -218,8 +218,11 @@ __device__ __forceinline__ void for_points(int nx, int ny, F f) {
   for_points(nx, ny, [&](const int p_, const int i_, const int j_, auto kin_)
 
 // ---------------------------------------------------------------------------- kernels
+// all == false: only the fields the PMA iteration itself reads next (J, A12; A11 / A22 go to the
+// LDS planes) -- the loop's last iteration writes the full set the caller reads afterwards
 __device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q, int ldq,
-                           const DropMesh& M, double* a11 = nullptr, double* a22 = nullptr) {
+                           const DropMesh& M, double* a11 = nullptr, double* a22 = nullptr,
+                           bool all = true) {
   const int nx = P.nx, ny = P.ny, NN = nx * ny;
   // compute_Q_spatial_ders (:696-711), J (:376) and the Laplace metric (:612-614): point-wise
   FOR_POINTS(NN) {
@@ -241,15 +244,19 @@ __device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q,
     const double q2y = op1<3, kIn>(C, q + j, i, ny, ldq) + t;
     const double qxy = (left || right || top || bottom) ? 0.0 : dxy<kIn>(C, q, i, j, nx, ny, ldq);
     const double J = q2x * q2y - qxy * qxy;
-    M.dksi[p] = qd;
-    M.deta[p] = qe;
-    M.d2ksi[p] = q2x;
-    M.d2eta[p] = q2y;
-    M.dksideta[p] = qxy;
+    if (all) {
+      M.dksi[p] = qd;
+      M.deta[p] = qe;
+      M.d2ksi[p] = q2x;
+      M.d2eta[p] = q2y;
+      M.dksideta[p] = qxy;
+    }
     M.J[p] = J;
     const double A11 = (qxy * qxy + q2y * q2y) / J, A22 = (qxy * qxy + q2x * q2x) / J;
-    M.A11[p] = A11;
-    M.A22[p] = A22;
+    if (all) {
+      M.A11[p] = A11;
+      M.A22[p] = A22;
+    }
     if (a11) {
       a11[i * ldq + j] = A11;
       a22[i * ldq + j] = A22;
@@ -806,7 +813,7 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
       // compute_Q_spatial_ders + J (:595-596) from q staged in L0; A11 -> L1, A22 -> L2
       FOR_POINTS(NN) { L0[i_ * ld + j_] = q[p_]; });
       __syncthreads();
-      mesh_stage(P, C, L0, ld, M, L1, L2);
+      mesh_stage(P, C, L0, ld, M, L1, L2, it == loops - 1);
       __syncthreads();
       mark(0);
       // compute_u_spatial_ders (:597) from u staged in L0
@@ -814,8 +821,10 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
       __syncthreads();
       uders_stage(P, C, M, CPlane(L0, ld), Plane{S.t1, nx}, Plane{S.t2, nx});
       __syncthreads();
+      // (u_xx / u_yy of the iteration's mesh are not read again: only the monitor is kept)
       lap_pressure_stage(P, C, M, CPlane(L0, ld), CPlane(L1, ld), CPlane(L2, ld),
-                         CPlane(S.t1, nx), CPlane(S.t2, nx), S.A, S.B, S.ud, Plane{S.p, nx});
+                         CPlane(S.t1, nx), CPlane(S.t2, nx), nullptr, nullptr, S.ud,
+                         Plane{S.p, nx});
       __syncthreads();
       FOR_POINTS(NN) { L0[i_ * ld + j_] = S.ud[p_]; });
       mark(1);
