@@ -52,10 +52,13 @@ hipError_t drop_rhs_launch(const DropParams& P, const double* uval, DropMesh M, 
 // residual(w, F, dt) (:435-450) at w = x + alpha*y (y may be null).
 //   mode 0: out = R(w); also xt <- w (if non-null) and partial[0..2] = sum R^2, max|R|, max|w|
 //   mode 1: out = (R(w) - f0) / sc  (the finite-difference JVP of KrylovJacobian.matvec)
+// znorm2 (optional, device): y is a raw basis vector whose |y|^2 is there; the kernel takes
+// sc = omega / |v|, alpha = sc / |y| (v = y / |y|) from it instead of the arguments.
 hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, const double* x,
                              const double* y, double alpha, const double* uval, const double* F,
                              double dt, int mode, const double* f0, double sc, double* out,
-                             double* xt, double* partial, hipStream_t s);
+                             double* xt, double* partial, hipStream_t s,
+                             const double* znorm2 = nullptr, double omega = 0.0);
 
 // compute_U2 (:413-423): u = eps + sum_d (1-eps) H2(G2(|x - x_d|, R_d), R_d, V_d) at the node
 // coordinates x = (M.dksi, M.deta); `drops` holds ndrops (x, y, R, V) quadruples (by value).
@@ -86,7 +89,8 @@ struct MemsParams {
 hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh M, DropScratch S,
                              const double* x, const double* y, double alpha, const double* uval,
                              const double* cn, int mode, const double* f0, double sc, double* out,
-                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s);
+                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s,
+                             const double* znorm2 = nullptr, double omega = 0.0);
 
 // Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
 // Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the four DCT operands of the MFMA path in

@@ -413,8 +413,17 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, 
                                                         const double* uval, const double* F,
                                                         double dt, int mode, const double* f0,
                                                         double sc, double* out, double* xt,
-                                                        double* partial) {
+                                                        double* partial, const double* znorm2,
+                                                        double omega) {
   const Coefs& C = Ck;
+  if (znorm2) {  // the FD step from the device value |z|^2 (KrylovJacobian.matvec, _nonlin.py:
+                 // 1505-1509, with v = z/|z|): the host's sc = omega/|v|, alpha = sc/|z|
+    const double hn = sqrt(*znorm2);
+    double sig = 1.0 / hn;
+    if (!isfinite(sig)) sig = 1.0;
+    sc = omega / (sig * hn);
+    alpha = sc * sig;
+  }
   coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, ld = kLds ? (nx | 1) : nx;
   extern __shared__ double lds[];
@@ -498,8 +507,16 @@ __global__ void __launch_bounds__(DB) mems_resid_kernel(DropParams P, Coefs Ck, 
                                                         const double* uval, const double* cn,
                                                         int mode, const double* f0, double sc,
                                                         double* out, double* xt, double* uxx,
-                                                        double* uyy, double* partial) {
+                                                        double* uyy, double* partial,
+                                                        const double* znorm2, double omega) {
   const Coefs& C = Ck;
+  if (znorm2) {  // the FD step from the device value |y|^2 (as drop_resid_kernel)
+    const double hn = sqrt(*znorm2);
+    double sig = 1.0 / hn;
+    if (!isfinite(sig)) sig = 1.0;
+    sc = omega / (sig * hn);
+    alpha = sc * sig;
+  }
   coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, ld = kLds ? (nx | 1) : nx;
   extern __shared__ double lds[];
@@ -916,7 +933,8 @@ hipError_t drop_rhs_launch(const DropParams& P, const double* uval, DropMesh M, 
 hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, const double* x,
                              const double* y, double alpha, const double* uval, const double* F,
                              double dt, int mode, const double* f0, double sc, double* out,
-                             double* xt, double* partial, hipStream_t s) {
+                             double* xt, double* partial, hipStream_t s, const double* znorm2,
+                             double omega) {
   if (!shape_ok(P)) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
   static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
@@ -926,10 +944,10 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(drop_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S,
-                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega);
   } else {
     hipLaunchKernelGGL(drop_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S,
-                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial);
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega);
   }
   return hipGetLastError();
 }
@@ -945,7 +963,8 @@ hipError_t drop_u2_launch(const DropParams& P, DropMesh M, const DropSet& drops,
 hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh M, DropScratch S,
                              const double* x, const double* y, double alpha, const double* uval,
                              const double* cn, int mode, const double* f0, double sc, double* out,
-                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s) {
+                             double* xt, double* uxx, double* uyy, double* partial, hipStream_t s,
+                             const double* znorm2, double omega) {
   if (!shape_ok(P) || mode < 0 || mode > 2) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
   static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
@@ -955,10 +974,12 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(mems_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), Mp,
-                       M, S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial);
+                       M, S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial, znorm2,
+                       omega);
   } else {
     hipLaunchKernelGGL(mems_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), Mp, M,
-                       S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial);
+                       S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial, znorm2,
+                       omega);
   }
   return hipGetLastError();
 }

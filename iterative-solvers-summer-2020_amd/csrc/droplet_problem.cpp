@@ -82,6 +82,14 @@ int DropletProblem::jvp(const double* x0, const double* G0, const double* z, dou
   });
 }
 
+int DropletProblem::jvp_dev(const double* x0, const double* G0, const double* z,
+                            const double* znorm2, double omega, double* w) {
+  return E_.launch(K_USERF, 0.0, [&] {
+    return drop_resid_launch(P_, M_, S_, x0, z, 0.0, uval, F, dt_, 1, G0, 1.0, w, nullptr, nullptr,
+                             E_.s, znorm2, omega);
+  });
+}
+
 // ============================================================================================
 // DropletStepper
 // ============================================================================================

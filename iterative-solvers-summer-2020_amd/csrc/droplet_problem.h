@@ -21,6 +21,11 @@ class DropletProblem : public Problem {
            double red[3]) override;
   int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
           double* w) override;
+  // the FD step from the device norm of the raw basis vector: no host round trip between the
+  // update of step j and the JVP of step j+1 (which the solver then issues speculatively)
+  bool has_dev_scale() const override { return true; }
+  int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
+              double omega, double* w) override;
   const DropMesh& mesh() const { return M_; }
   const DropScratch& scratch() const { return S_; }
   const DropParams& params() const { return P_; }

@@ -40,6 +40,14 @@ int MemsProblem::jvp(const double* x0, const double* G0, const double* z, double
   });
 }
 
+int MemsProblem::jvp_dev(const double* x0, const double* G0, const double* z,
+                         const double* znorm2, double omega, double* w) {
+  return E_.launch(K_USERF, 0.0, [&] {
+    return mems_resid_launch(P_, Mp_, M_, S_, x0, z, 0.0, uval, F, 1, G0, 1.0, w, nullptr, nullptr,
+                             nullptr, nullptr, E_.s, znorm2, omega);
+  });
+}
+
 MemsStepper::MemsStepper(const DropParams& Pp, const MemsParams& Mp, double epsilon,
                          const nk_opts& o, hipStream_t s)
     : opts(o), E(int64_t(Pp.nx) * Pp.ny, nullptr, s, o.profile != 0, 16), P(E, Pp, Mp),

@@ -19,6 +19,8 @@ class MemsProblem final : public DropletProblem {
            double red[3]) override;
   int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
           double* w) override;
+  int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
+              double omega, double* w) override;
 
  private:
   MemsParams Mp_;
