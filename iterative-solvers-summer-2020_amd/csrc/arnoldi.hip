@@ -55,6 +55,10 @@ namespace {
 constexpr int kSW = 64;       // columns per wave (one per lane)
 constexpr int WPB = ARN_WPB;  // waves per block (the packed halo loads carry 16 * WPB entries)
 static_assert(WPB * kSW == kEdgeW, "edge arrays are laid out for the fused kernel's blocks");
+// waves per block of the mailbox instantiation: it reads no edge arrays, and its halos cost a
+// record per block side, so narrower blocks (less LDS lag per block, 2-wave barriers) pay:
+// nv 24 0.602-0.610 -> 0.618-0.619 of 8 TB/s with 2 waves (profiles/r02_arnoldi_ab.md)
+constexpr int kMbWPB = 2;
 
 __device__ __forceinline__ double applyL13(const SHCoef& k, double c, double a1, double dg,
                                            double a2) {
@@ -248,8 +252,8 @@ __device__ __forceinline__ double dpp_down(double x) {
 // sums each half's entries and adds the other half's sum (v_permlane32_swap); both halves then
 // hold v, y and w' of the wave's 64 columns, and each half takes the dot products of its own
 // entries (half 0 also w'.v, v.v, w'.w').
-template <int NV, bool EXT, int PF, bool NT, bool MB>
-__global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) {
+template <int NV, bool EXT, int PF, bool NT, bool MB, int WB>
+__global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
   double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
 #pragma unroll
@@ -261,11 +265,11 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   constexpr int NB = (NV + 1) / 2;         // loads holding basis entries
   constexpr int EX = NV + 1, EZ = NV + 2;  // entries of x0, z
   // lag rows r, r+1 of this lane's basis entries and of x0, for row r's dot products / stencil
-  __shared__ dv2 lag[WPB][2][NB + 1][64];
+  __shared__ dv2 lag[WB][2][NB + 1][64];
   // per row (parity slot): u on columns 0, 1, 62, 63 of every wave; the waves' partial sums of v
   // on the block's four halo columns
-  __shared__ double edge[2][WPB][4];
-  __shared__ double hpart[2][WPB][4];
+  __shared__ double edge[2][WB][4];
+  __shared__ double hpart[2][WB][4];
   const int lane = threadIdx.x & 63;
   const int hf = lane >> 5, l = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -274,18 +278,18 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const int64_t b = blockIdx.x;
   const int64_t bpx = gridDim.x / 8;  // grid is a multiple of 8
   const int64_t L = (b % 8) * bpx + b / 8;
-  const int64_t ngroups = (A.strips + WPB - 1) / WPB;  // a block = WPB adjacent strips
+  const int64_t ngroups = (A.strips + WB - 1) / WB;  // a block = WB adjacent strips
   if (L >= ngroups * A.nbands) return;                 // whole blocks only
   const int64_t band = L / ngroups, grp = L % ngroups;
-  const int64_t gw = L * WPB + wid;  // partial-sum column of this wave
+  const int64_t gw = L * WB + wid;  // partial-sum column of this wave
   const int64_t nx = A.nx, ny = A.ny;
-  const int64_t B0 = grp * WPB * kSW;        // the block's first column
+  const int64_t B0 = grp * WB * kSW;        // the block's first column
   const int64_t c = B0 + wid * kSW + 2 * l;  // columns past nx compute wrapped columns, masked
   const int64_t col = c % nx;                // nx even: c and c+1 wrap together
   const bool own = c < nx;
-  // block halo: h = 0, 1 -> columns B0-2, B0-1; h = 2, 3 -> B0 + WPB*64, +1
+  // block halo: h = 0, 1 -> columns B0-2, B0-1; h = 2, 3 -> B0 + WB*64, +1
   const int hh = lane & 3;
-  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WPB * kSW - 2 + hh;
+  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WB * kSW - 2 + hh;
   const int64_t hcol = ((hc % nx) + nx) % nx;
   const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
   const int64_t r0 = A.r_begin + band * A.RY;
@@ -314,13 +318,13 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     ep[k] = hf ? src(e1) : src(e0);
     ecf[k] = hf ? (2 * k + 1 < NE ? cof(e1) : 0.0) : cof(e0);
   }
-  // packed block-halo loads (8 B per lane), shared by the WPB waves: lane L of wave w fetches
-  // halo column L%4 of entry e = w + WPB*(L/4) of [V_0 .. V_{NV-1}, w] with coefficient c_e (tau
+  // packed block-halo loads (8 B per lane), shared by the WB waves: lane L of wave w fetches
+  // halo column L%4 of entry e = w + WB*(L/4) of [V_0 .. V_{NV-1}, w] with coefficient c_e (tau
   // for w); lanes past the list repeat entry w's address (same line) with coefficient 0
   const double* hp;
   double hcf;
   {
-    const int e = wid + WPB * (lane >> 2);
+    const int e = wid + WB * (lane >> 2);
     const double* p = (wid < NV) ? A.V[wid < NV ? wid : 0] : A.w;
     double cf = 0.0;
 #pragma unroll
@@ -337,7 +341,7 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   const bool useE = A.E[0] != nullptr;
   const double* hE;
   {
-    const int e = wid + WPB * (lane >> 2);
+    const int e = wid + WB * (lane >> 2);
     const double* p = A.E[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) p = (e == j) ? A.E[j] : p;
@@ -374,16 +378,16 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
   };
 
   // mailbox (see "Mailbox" above): wave 0's lanes l == 0 hold the block's first column pair and
-  // need its left halo pair, wave WPB-1's lanes l == 31 its last pair and the right halo pair
-  constexpr int BW = WPB * kSW;
+  // need its left halo pair, wave WB-1's lanes l == 31 its last pair and the right halo pair
+  constexpr int BW = WB * kSW;
   constexpr bool mb = MB && !EXT;  // a separate instantiation: the plain one has none of it
   const int64_t mbT = A.RY + 8;             // records per block and side (rows pushed <= RY + 7)
   const __amdgpu_buffer_rsrc_t rmb = rsrc(A.mb, mb ? A.mb_cap : 0);
   const uint64_t tag = A.mb_tag;
-  const bool needL = mb && wid == 0 && l == 0, needR = mb && wid == WPB - 1 && l == 31;
+  const bool needL = mb && wid == 0 && l == 0, needR = mb && wid == WB - 1 && l == 31;
   const int64_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
   const int nside = needL ? 1 : 0;  // my left halo = the left neighbour's right-edge records
-  const bool prod = mb && ((wid == 0 && lane == 0) || (wid == WPB - 1 && lane == 31));
+  const bool prod = mb && ((wid == 0 && lane == 0) || (wid == WB - 1 && lane == 31));
   const int pside = (wid == 0 && lane == 0) ? 0 : 1;
   const int64_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;  // the halo pair's columns
   // this lane stopped polling (a neighbour was not there in time; mb_recompute: test switch)
@@ -558,11 +562,11 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     } else if constexpr (!mb) {
       hz = 0.0;
 #pragma unroll
-      for (int w = 0; w < WPB; ++w) hz += hpart[slot][w][hh];  // fixed order: deterministic
+      for (int w = 0; w < WB; ++w) hz += hpart[slot][w][hh];  // fixed order: deterministic
     }
     // lanes 0..3: block halo columns -2, -1, +0, +1
     const double yh = s.own ? hz : s.hx;  // u on the halo columns
-    const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WPB - 1) ? wid + 1 : WPB - 1;
+    const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WB - 1) ? wid + 1 : WB - 1;
 #if ARN_SELECT
     // both candidates are read unconditionally (a uniform select, no branch around LDS reads)
     const double el2 = edge[slot][wl][2], el1 = edge[slot][wl][3];
@@ -570,12 +574,12 @@ __global__ void __launch_bounds__(64 * WPB) arnoldi_kernel(const ArnoldiArgs A) 
     const double hl2 = readlane(yh, 0), hl1 = readlane(yh, 1);
     const double hr1 = readlane(yh, 2), hr2 = readlane(yh, 3);
     const double yl2 = (wid == 0) ? hl2 : el2, yl1 = (wid == 0) ? hl1 : el1;
-    const double yr1 = (wid == WPB - 1) ? hr1 : er1, yr2 = (wid == WPB - 1) ? hr2 : er2;
+    const double yr1 = (wid == WB - 1) ? hr1 : er1, yr2 = (wid == WB - 1) ? hr2 : er2;
 #else
     const double yl2 = (wid == 0) ? readlane(yh, 0) : edge[slot][wl][2];
     const double yl1 = (wid == 0) ? readlane(yh, 1) : edge[slot][wl][3];
-    const double yr1 = (wid == WPB - 1) ? readlane(yh, 2) : edge[slot][wr][0];
-    const double yr2 = (wid == WPB - 1) ? readlane(yh, 3) : edge[slot][wr][1];
+    const double yr1 = (wid == WB - 1) ? readlane(yh, 2) : edge[slot][wr][0];
+    const double yr2 = (wid == WB - 1) ? readlane(yh, 3) : edge[slot][wr][1];
 #endif
     // neighbours inside the half: lane l-1 holds columns 2l-2, 2l-1 (the lanes whose neighbour
     // is across the half boundary take the edge values below)
@@ -1153,54 +1157,65 @@ struct Occ {
 // `nwb` waves of `cw` columns each; bands of >= 8 rows, and no more partial columns than the
 // caller's buffer holds.  `occ` = that kernel's occupancy.
 template <int NV, class K>
-hipError_t launch_grid(K kern, const Occ& occ, K kern_mb, const Occ& occ_mb, bool has_mb, int nwb,
-                       int cw, ArnoldiArgs A, hipStream_t s,
-                       int64_t* nwaves) {
-  if (occ.ncu == 0) return hipErrorUnknown;
+hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& occ_mb, int nwb_mb,
+                       bool has_mb, int cw, ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
+  if (occ.ncu == 0 || occ_mb.ncu == 0) return hipErrorUnknown;
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
   const int64_t strips = (A.nx + cw - 1) / cw;
   const int64_t rb = A.r_begin, re = (A.r_end >= 0) ? A.r_end : A.ny;
   if (rb < 0 || re > A.ny || re <= rb) return hipErrorInvalidValue;
   const int64_t rows = re - rb;
-  const int64_t ncu_use = (occ.ncu - A.reserve_cus > 0) ? occ.ncu - A.reserve_cus : 1;
-  const int64_t target = ncu_use * occ.blocks_per_cu * nwb * (rounds > 0 ? rounds : 1);
-  const int64_t wpr = (strips + nwb - 1) / nwb * nwb;  // waves per band (whole blocks)
-  int64_t nbands = target / wpr;
-  const int64_t cap_bands = A.partial_cap / ((2 * int64_t(NV) + 3) * wpr);
-  if (nbands > cap_bands) nbands = cap_bands;
-  if (nbands > rows / 8) nbands = rows / 8;
-  if (nbands < 1) nbands = 1;
-  // the mailbox: whole periodic rows of >= 2 blocks; a multiple of 8 bands, so that each XCD's
-  // contiguous run of blocks (the blockIdx mapping in the kernels) holds whole bands
-  const int64_t ngr = (strips + nwb - 1) / nwb;
-  bool mbox = has_mb && A.mb && !A.z && A.nx % (int64_t(nwb) * cw) == 0 && ngr >= 2 && rb == 0 &&
-              re == A.ny && occ_mb.blocks_per_cu == occ.blocks_per_cu;
-  if (mbox && nbands >= 8) nbands -= nbands % 8;
-  const int64_t RY = (rows + nbands - 1) / nbands;
-  nbands = (rows + RY - 1) / RY;
-  const int64_t nw = wpr * nbands;
+  // bands of one resident round of `w`-wave blocks at occupancy `o`; with the mailbox a
+  // multiple of 8 bands, so that each XCD's contiguous run of blocks (the blockIdx mapping in
+  // the kernels) holds whole bands
+  struct Plan {
+    int64_t nbands, RY, wpr, nw;
+  };
+  auto plan = [&](const Occ& o, int w, bool mbox) {
+    const int64_t ncu_use = (o.ncu - A.reserve_cus > 0) ? o.ncu - A.reserve_cus : 1;
+    const int64_t target = ncu_use * o.blocks_per_cu * w * (rounds > 0 ? rounds : 1);
+    Plan p;
+    p.wpr = (strips + w - 1) / w * w;  // waves per band (whole blocks)
+    p.nbands = target / p.wpr;
+    const int64_t cap_bands = A.partial_cap / ((2 * int64_t(NV) + 3) * p.wpr);
+    if (p.nbands > cap_bands) p.nbands = cap_bands;
+    if (p.nbands > rows / 8) p.nbands = rows / 8;
+    if (p.nbands < 1) p.nbands = 1;
+    if (mbox && p.nbands >= 8) p.nbands -= p.nbands % 8;
+    p.RY = (rows + p.nbands - 1) / p.nbands;
+    p.nbands = (rows + p.RY - 1) / p.RY;
+    p.nw = p.wpr * p.nbands;
+    return p;
+  };
+  // the mailbox: whole periodic rows of >= 2 of its blocks, records for every block
+  const int64_t ngr = (strips + nwb_mb - 1) / nwb_mb;
+  bool mbox = has_mb && A.mb && !A.z && A.nx % (int64_t(nwb_mb) * cw) == 0 && ngr >= 2 &&
+              rb == 0 && re == A.ny;
+  Plan P = plan(occ_mb, nwb_mb, true);
+  if (mbox && ngr * P.nbands * (P.RY + 8) * 8 > A.mb_cap) mbox = false;
+  if (!mbox) P = plan(occ, nwb, false);
+  const int w = mbox ? nwb_mb : nwb;
   if (A.plan_only) {
-    *nwaves = nw;
+    *nwaves = P.nw;
     return hipSuccess;
   }
-  if (A.pstride == 0) A.pstride = nw;
-  if (A.pcol0 < 0 || A.pcol0 + nw > A.pstride ||
+  if (A.pstride == 0) A.pstride = P.nw;
+  if (A.pcol0 < 0 || A.pcol0 + P.nw > A.pstride ||
       A.pstride * (2 * int64_t(NV) + 3) > A.partial_cap)
     return hipErrorInvalidValue;
   A.strips = int(strips);
-  A.nbands = int(nbands);
-  A.RY = int(RY);
-  if (mbox && ngr * nbands * (RY + 8) * 8 > A.mb_cap) mbox = false;  // records for every block
+  A.nbands = int(P.nbands);
+  A.RY = int(P.RY);
   if (mbox) {
     kern = kern_mb;  // the mailbox instantiation
     g_mbox_launches.fetch_add(1, std::memory_order_relaxed);
   } else {
     A.mb = nullptr;
   }
-  int64_t blocks = (nw + nwb - 1) / nwb;
+  int64_t blocks = (P.nw + w - 1) / w;
   blocks = (blocks + 7) / 8 * 8;
-  *nwaves = nw;
-  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * nwb), 0, s, A);
+  *nwaves = P.nw;
+  hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * w), 0, s, A);
   return hipGetLastError();
 }
 
@@ -1221,12 +1236,13 @@ Occ query_occ(K kern, int threads) {
 
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
-  auto kern = arnoldi_kernel<NV, EXT, PF, NT, false>;
-  auto kern_mb = arnoldi_kernel<NV, EXT, PF, NT, !EXT>;  // EXT: no mailbox, the same kernel
+  constexpr int WM = EXT ? WPB : kMbWPB;
+  auto kern = arnoldi_kernel<NV, EXT, PF, NT, false, WPB>;
+  auto kern_mb = arnoldi_kernel<NV, EXT, PF, NT, !EXT, WM>;  // EXT: no mailbox, the same kernel
   if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
   static const Occ occ = query_occ(kern, 64 * WPB);
-  static const Occ occ_mb = query_occ(kern_mb, 64 * WPB);
-  return launch_grid<NV>(kern, occ, kern_mb, occ_mb, !EXT, WPB, kSW, A, s, nwaves);
+  static const Occ occ_mb = query_occ(kern_mb, 64 * WM);
+  return launch_grid<NV>(kern, occ, WPB, kern_mb, occ_mb, WM, !EXT, kSW, A, s, nwaves);
 }
 
 constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
@@ -1236,7 +1252,7 @@ hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   // (4096^2, one box: n4 0.63 vs 0.55, n12 0.64 vs 0.63, n18 0.62 vs 0.57 of 8 TB/s)
   auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW, false>;
   static const Occ occ = query_occ(kern, 64 * kWideW);
-  return launch_grid<NV>(kern, occ, kern, occ, false, kWideW, kWW, A, s, nwaves);
+  return launch_grid<NV>(kern, occ, kWideW, kern, occ, kWideW, false, kWW, A, s, nwaves);
 }
 
 template <int NV, bool EXT>

@@ -244,12 +244,12 @@ def test_device_control_default_tolerance():
 
 def _mbox_expected(nv, nx):
     """Whether the fused kernel's grid takes the mailbox: the vector-pair layout (nv >= 19;
-    the wide layout keeps its packed halo loads) with nx a multiple of its 256-column blocks and
-    two blocks per band at least."""
-    return nv >= 19 and nx % 256 == 0 and nx // 256 >= 2
+    the wide layout keeps its packed halo loads) with nx a multiple of its mailbox instantiation's
+    128-column blocks and two blocks per band at least."""
+    return nv >= 19 and nx % 128 == 0 and nx // 128 >= 2
 
 
-@pytest.mark.parametrize("ny,nx", [(64, 1024), (40, 512), (24, 2048)])
+@pytest.mark.parametrize("ny,nx", [(64, 1024), (40, 512), (24, 2048), (32, 384)])
 @pytest.mark.parametrize("nv", [1, 6, 18, 19, 27, 35])
 def test_fused_kernel_mailbox(ny, nx, nv, monkeypatch):
     """Block halos through the mailbox (arnoldi.hip "Mailbox": the blocks of a band publish u on
