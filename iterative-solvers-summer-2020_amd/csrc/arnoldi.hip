@@ -58,7 +58,10 @@ static_assert(WPB * kSW == kEdgeW, "edge arrays are laid out for the fused kerne
 // waves per block of the mailbox instantiation: it reads no edge arrays, and its halos cost a
 // record per block side, so narrower blocks (less LDS lag per block, 2-wave barriers) pay:
 // nv 24 0.602-0.610 -> 0.618-0.619 of 8 TB/s with 2 waves (profiles/r02_arnoldi_ab.md)
-constexpr int kMbWPB = 2;
+#ifndef ARN_MBWPB
+#define ARN_MBWPB 2
+#endif
+constexpr int kMbWPB = ARN_MBWPB;
 
 __device__ __forceinline__ double applyL13(const SHCoef& k, double c, double a1, double dg,
                                            double a2) {
@@ -1245,13 +1248,25 @@ hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   return launch_grid<NV>(kern, occ, WPB, kern_mb, occ_mb, WM, !EXT, kSW, A, s, nwaves);
 }
 
-constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
+#ifndef ARN_WIDEW
+#define ARN_WIDEW 4
+#endif
+#ifndef ARN_WIDE_MB
+#define ARN_WIDE_MB 0
+#endif
+constexpr int kWideW = ARN_WIDEW;  // waves per block of the wide layout (512 columns)
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   // no mailbox instantiation: with 512-column blocks the packed halo is the cheaper one
   // (4096^2, one box: n4 0.63 vs 0.55, n12 0.64 vs 0.63, n18 0.62 vs 0.57 of 8 TB/s)
   auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW, false>;
   static const Occ occ = query_occ(kern, 64 * kWideW);
+  if constexpr (ARN_WIDE_MB != 0) {  // experiment: a mailbox instantiation for the wide layout
+    constexpr int WM = ARN_WIDE_MB;
+    auto kern_mb = arnoldi_wide_kernel<NV, EXT, PF, NT, WM, !EXT>;
+    static const Occ occ_mb = query_occ(kern_mb, 64 * WM);
+    return launch_grid<NV>(kern, occ, kWideW, kern_mb, occ_mb, WM, !EXT, kWW, A, s, nwaves);
+  }
   return launch_grid<NV>(kern, occ, kWideW, kern, occ, kWideW, false, kWW, A, s, nwaves);
 }
 
