@@ -282,6 +282,42 @@ def jvp_isolated(n, h, r, k, g, x0, jvp, reps=20):
             "source": f"{reps} back-to-back launches on resident {n}^2 inputs after the timed region"}
 
 
+def copy_bandwidth(n, reps=20):
+    """This box's streaming rate, measured after the timed region so roofline fractions can be
+    compared across boxes (their HBM spread is ~15 %): n^2 fp64 device-to-device copies (read one
+    vector, write one: 16 B/pt) by nk_stream_copy (16-KB chunks per block, non-temporal; the
+    guide's float4-copy pattern, ~6.3 TB/s) and, for reference, torch's copy_; alternating between
+    two buffer pairs so the 4 x n^2 working set (537 MB at 4096^2) exceeds the 256 MB Infinity
+    Cache; HIP events on the current stream.  peak_measured = the faster of the two."""
+    import torch
+
+    import nkhip
+    bufs = [torch.empty(n * n, dtype=torch.float64, device="cuda") for _ in range(4)]
+    for b_ in bufs:
+        b_.normal_()
+
+    def rate(fn):
+        for i in range(4):
+            fn(bufs[2 * (i % 2)], bufs[2 * (i % 2) + 1])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for i in range(reps):
+            fn(bufs[2 * (i % 2)], bufs[2 * (i % 2) + 1])
+        b.record()
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / reps
+        return round(16.0 * n * n / (us * 1e-6) / 1e9, 1), round(us, 2)
+
+    lib_gbs, lib_us = rate(lambda s_, d_: nkhip.stream_copy(s_, out=d_))
+    torch_gbs, _ = rate(lambda s_, d_: d_.copy_(s_))
+    del bufs
+    return {"GB/s": max(lib_gbs, torch_gbs), "nk_stream_copy_GB/s": lib_gbs,
+            "nk_stream_copy_avg_us": lib_us, "torch_copy_GB/s": torch_gbs,
+            "what": f"{n}^2 fp64 copies (16 B/pt), {reps} reps over two buffer pairs, HIP events, "
+                    "after the timed region"}
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "latest_traffic.json")
     try:
@@ -446,6 +482,15 @@ def main():
         }
         if world == 1:
             out["jvp_roofline_isolated"] = jvp_isolated(n, h, r, k, g, a, args.jvp)
+        # the box's measured streaming rate beside the 8 TB/s spec: frac_of_measured makes the
+        # fractions comparable across boxes
+        cb = copy_bandwidth(n)
+        out["copy_bandwidth"] = cb
+        for key in ("roofline", "jvp_roofline", "jvp_roofline_isolated"):
+            rl = out.get(key)
+            if rl:
+                rl["peak_measured"] = cb["GB/s"]
+                rl["frac_of_measured"] = round(rl["achieved"] / cb["GB/s"], 4)
         if want_cpu:
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
             rec, u_cpu = cpu_baseline(n, h, k, r, g, u_start, fe)

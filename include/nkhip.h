@@ -35,6 +35,11 @@ extern "C" {
 #define NK_ECOMM (-3)
 #define NK_ENOMEM (-4)
 
+/* Layout version of the structs and signatures below.  nk_stats is written whole by the library
+ * (sizeof(nk_stats) bytes): a caller built against another version must not pass its own
+ * struct.  3: nk_stats gained n_backtrack, step_min, n_device_steps (round 2); nk_sh_step_log. */
+#define NKHIP_ABI_VERSION 3
+
 #define NK_JVP_FD 0       /* KrylovJacobian.matvec finite difference (scipy-faithful) */
 #define NK_JVP_ANALYTIC 1 /* exact J v = v/k - (L v + (2 g u - 3 u^2) v)/2 */
 
@@ -82,6 +87,8 @@ typedef struct nk_comm nk_comm;
 typedef struct nk_sh nk_sh;
 
 const char* nk_version(void);
+/* NKHIP_ABI_VERSION of the library: a binding checks it against the header it was built from. */
+int nk_abi_version(void);
 int nk_opts_default(nk_opts* o);
 const char* nk_status_string(int code);
 
@@ -164,6 +171,11 @@ int nk_mdot(const double* const* V_dev, int32_t m, const double* w_dev, int64_t 
 int nk_maxpy(const double* const* V_dev, const double* coef, int32_t m, double* y_dev, int64_t n,
              void* stream);
 
+/* dst = src (n doubles, n even, 16-B aligned), streamed in 16-KB chunks per block with
+ * non-temporal loads and stores.  No reference counterpart: the bench's probe of the box's
+ * achievable HBM streaming rate (roofline.peak_measured), the ~6.3 TB/s of a float4 copy. */
+int nk_stream_copy(const double* src_dev, double* dst_dev, int64_t n, void* stream);
+
 /* ---------------- communicators (row-slab decomposition over RCCL / xGMI) ---------------- */
 int nk_comm_unique_id_bytes(void);
 int nk_comm_get_unique_id(void* out);
@@ -194,6 +206,11 @@ int nk_sh_set_opts(nk_sh* s, const nk_opts* opts);
 /* Copies up to `max` per-kernel-class records; returns the number of classes. */
 int nk_sh_kernel_profile(nk_sh* s, nk_kprof* out, int32_t max);
 int nk_sh_reset_profile(nk_sh* s);
+/* The accepted line-search step s of every Newton iteration of the last nk_sh_step
+ * (scalar_search_armijo's result inside _nonlin_line_search, scipy/optimize/_nonlin.py:294-314;
+ * the `step %g` of the reference's verbose line, sh_scipy_nk.py:61): copies up to `max` of them
+ * to `steps` (host) and returns how many there were. */
+int nk_sh_step_log(nk_sh* s, double* steps, int32_t max);
 int64_t nk_sh_workspace_bytes(nk_sh* s);
 
 /* ---------------- generic drop-in: newton_krylov(F, xin) over a device residual ---------------- */

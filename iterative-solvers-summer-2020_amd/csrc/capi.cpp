@@ -59,7 +59,8 @@ struct nk_sh {
 
 extern "C" {
 
-const char* nk_version(void) { return "nkhip 0.1.0 (gfx950)"; }
+const char* nk_version(void) { return "nkhip 0.3.0 (gfx950)"; }
+int nk_abi_version(void) { return NKHIP_ABI_VERSION; }
 
 int nk_opts_default(nk_opts* o) {
   if (!o) return NK_EINVAL;
@@ -351,6 +352,11 @@ int nk_maxpy(const double* const* V, const double* coef, int32_t m, double* y, i
   return hip_rc(combo_launch(y, y, 1.0, P, m, n, nullptr, S(stream), &nb));
 }
 
+int nk_stream_copy(const double* src, double* dst, int64_t n, void* stream) {
+  if (!src || !dst || n < 0) return NK_EINVAL;
+  return hip_rc(stream_copy_launch(src, dst, n, S(stream)));
+}
+
 // ------------------------------------------------------------------------------ comms
 int nk_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
 int nk_comm_get_unique_id(void* out) { return out ? comm_get_unique_id(out) : NK_EINVAL; }
@@ -439,6 +445,13 @@ int nk_sh_reset_profile(nk_sh* s) {
   if (!s) return NK_EINVAL;
   s->E->reset_stats();
   return NK_OK;
+}
+
+int nk_sh_step_log(nk_sh* s, double* steps, int32_t max) {
+  if (!s || max < 0 || (max > 0 && !steps)) return NK_EINVAL;
+  const std::vector<double>& log = s->NK->step_log();
+  for (int32_t i = 0; i < max && size_t(i) < log.size(); ++i) steps[i] = log[i];
+  return int(log.size());
 }
 
 int64_t nk_sh_workspace_bytes(nk_sh* s) { return s ? s->E->bytes_allocated() : -1; }

@@ -376,6 +376,38 @@ hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, in
   return hipGetLastError();
 }
 
+namespace {
+// Streaming copy in contiguous 16-KB chunks per block (256 lanes x 4 x 16 B, all four loads in
+// flight before the first store; non-temporal both ways): the pattern that streams fastest on
+// this chip (scripts/micro/pattern2_bench.hip), used as the bench's per-box bandwidth probe.
+typedef double sdv2 __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256) stream_copy_kernel(const sdv2* __restrict__ src,
+                                                          sdv2* __restrict__ dst, int64_t n2) {
+  const int64_t base = int64_t(blockIdx.x) * 1024 + threadIdx.x;
+  sdv2 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n2) v[k] = __builtin_nontemporal_load(src + i);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n2) __builtin_nontemporal_store(v[k], dst + i);
+  }
+}
+
+}  // namespace
+
+hipError_t stream_copy_launch(const double* src, double* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (!al16(src) || !al16(dst) || n % 2) return hipErrorInvalidValue;
+  const int64_t n2 = n / 2;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(unsigned((n2 + 1023) / 1024)), dim3(256), 0, s,
+                     reinterpret_cast<const sdv2*>(src), reinterpret_cast<sdv2*>(dst), n2);
+  return hipGetLastError();
+}
+
 hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
                         int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

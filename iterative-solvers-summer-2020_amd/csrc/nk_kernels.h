@@ -111,6 +111,9 @@ hipError_t cg_update_launch(double* x, double* r, const double* p, const double*
 // d = (5U - Uo)^2 k/16 - g k U (sh_linearised.py:50)
 hipError_t shlin_diag_launch(const double* U, const double* Uo, double k, double g, double* d,
                              int64_t n, hipStream_t s);
+// dst = src, streamed in 16-KB chunks per block (the bench's per-box bandwidth probe); n even,
+// 16-B aligned
+hipError_t stream_copy_launch(const double* src, double* dst, int64_t n, hipStream_t s);
 hipError_t axpby_launch(double a, const double* x, double b, const double* y, double* out,
                         int64_t n, hipStream_t s);
 

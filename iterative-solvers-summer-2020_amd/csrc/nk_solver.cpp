@@ -94,42 +94,133 @@ Engine::~Engine() {
     hipEventDestroy(p.b);
   }
   for (auto e : free_ev_) hipEventDestroy(e);
-  if (own_pool_ && pool_) hipFree(pool_);
-  if (epool_) hipFree(epool_);
+  if (vmm_base_) {
+    vmm_free();  // the pool and its edge arrays
+  } else {
+    if (own_pool_ && pool_) hipFree(pool_);
+    if (epool_) hipFree(epool_);
+  }
   if (partial_) hipFree(partial_);
   if (dres_) hipFree(dres_);
   if (hres_) hipHostFree(hres_);
 }
 
+// The pool as `chunk`-sized physical allocations mapped back to back into a chunk-aligned
+// virtual range (hipMemCreate / hipMemMap): virtual and physical addresses then agree modulo the
+// chunk, so the page tables may use fragments up to the chunk size.
+int Engine::vmm_alloc(size_t bytes, size_t chunk) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return NK_EHIP;
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) !=
+          hipSuccess || gran == 0)
+    return NK_EHIP;
+  chunk = (chunk + gran - 1) / gran * gran;
+  const size_t total = (bytes + chunk - 1) / chunk * chunk;
+  if (hipMemAddressReserve(&vmm_base_, total, chunk, nullptr, 0) != hipSuccess) {
+    vmm_base_ = nullptr;
+    return NK_ENOMEM;
+  }
+  vmm_size_ = total;
+  vmm_chunk_ = chunk;
+  for (size_t off = 0; off < total; off += chunk) {
+    hipMemGenericAllocationHandle_t h;
+    if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+      vmm_free();
+      return NK_ENOMEM;
+    }
+    vmm_h_.push_back(h);
+    if (hipMemMap(static_cast<char*>(vmm_base_) + off, chunk, 0, h, 0) != hipSuccess) {
+      vmm_free();
+      return NK_EHIP;
+    }
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipMemSetAccess(vmm_base_, total, &acc, 1) != hipSuccess) {
+    vmm_free();
+    return NK_EHIP;
+  }
+  return NK_OK;
+}
+
+void Engine::vmm_free() {
+  if (!vmm_base_) return;
+  for (size_t i = 0; i < vmm_h_.size(); ++i) {
+    hipMemUnmap(static_cast<char*>(vmm_base_) + i * vmm_chunk_, vmm_chunk_);
+    hipMemRelease(vmm_h_[i]);
+  }
+  vmm_h_.clear();
+  hipMemAddressFree(vmm_base_, vmm_size_);
+  vmm_base_ = nullptr;
+  (void)hipGetLastError();
+}
+
 int Engine::alloc(int count, std::vector<double*>* out, void* external, int64_t external_bytes) {
   if (!partial_ || !dres_ || !hres_) return NK_ENOMEM;
   const int64_t bytes = sizeof(double) * npad * int64_t(count);
+  const bool edges = edge_ny_ > 0 && edge_nx_ > 0;
+  edge_n_ = edges ? edge_elems(edge_ny_, edge_nx_) : 0;
+  const int64_t eb = (sizeof(double) * edge_n_ * count + 255) / 256 * 256;
   if (external) {
     if (external_bytes < bytes || (reinterpret_cast<uintptr_t>(external) & 255u)) return NK_EINVAL;
     pool_ = static_cast<double*>(external);
     own_pool_ = false;
   } else {
-    if (hipMalloc(reinterpret_cast<void**>(&pool_), bytes) != hipSuccess) {
-      pool_ = nullptr;
-      return NK_ENOMEM;
+    // Large pools are mapped through the virtual memory API in 1-GB (64-MB) chunks rather than
+    // taken from hipMalloc: the streaming kernels ran up to 5 % apart on hipMalloc pools that
+    // differed only in where they landed (one process, several steppers, each stable over
+    // rounds: fused kernel 0.632-0.640 on three pools in four, 0.66-0.675 on the fourth), and
+    // 0.667-0.683 on every chunk-mapped pool (scripts/dbg/pool_placement.py, profiles/
+    // r03_pool_placement.md) -- consistent with page-table fragments limited by how the
+    // hipMalloc range's virtual and physical alignments happen to match, which the chunk-aligned
+    // mapping fixes.  The edge arrays share the mapping.  NKHIP_POOL_ALLOC=malloc: hipMalloc.
+    const char* how = std::getenv("NKHIP_POOL_ALLOC");
+    const bool vmm = !(how && std::strcmp(how, "malloc") == 0) && bytes + eb >= (int64_t(1) << 28);
+    int rc = NK_ENOMEM;
+    if (vmm) {
+      const size_t chunk = size_t(1) << ((bytes + eb >= (int64_t(1) << 33)) ? 30 : 26);
+      rc = vmm_alloc(size_t(bytes + eb), chunk);
+      if (rc == NK_OK) {
+        pool_ = static_cast<double*>(vmm_base_);
+        if (edges) epool_ = pool_ + bytes / int64_t(sizeof(double));
+      }
+    }
+    if (rc != NK_OK) {  // small pools, or the mapping failed: plain allocations
+      (void)hipGetLastError();
+      if (hipMalloc(reinterpret_cast<void**>(&pool_), bytes) != hipSuccess) {
+        pool_ = nullptr;
+        return NK_ENOMEM;
+      }
+      if (edges && hipMalloc(reinterpret_cast<void**>(&epool_), eb) != hipSuccess) {
+        epool_ = nullptr;
+        return NK_ENOMEM;
+      }
     }
     own_pool_ = true;
-    bytes_ += bytes;
+    bytes_ += bytes + (edges ? eb : 0);
   }
-  if (hipMemsetAsync(pool_, 0, bytes, s) != hipSuccess) return NK_EHIP;
-  out->resize(count);
-  for (int i = 0; i < count; ++i) (*out)[i] = pool_ + npad * i;
-  pool_count_ = count;
-  if (edge_ny_ > 0 && edge_nx_ > 0) {
-    edge_n_ = edge_elems(edge_ny_, edge_nx_);
-    const int64_t eb = sizeof(double) * edge_n_ * count;
+  if (external && edges) {
     if (hipMalloc(reinterpret_cast<void**>(&epool_), eb) != hipSuccess) {
       epool_ = nullptr;
       return NK_ENOMEM;
     }
     bytes_ += eb;
-    if (hipMemsetAsync(epool_, 0, eb, s) != hipSuccess) return NK_EHIP;
   }
+  if (hipMemsetAsync(pool_, 0, bytes, s) != hipSuccess) return NK_EHIP;
+  if (epool_ && hipMemsetAsync(epool_, 0, eb, s) != hipSuccess) return NK_EHIP;
+  if (std::getenv("NKHIP_DEBUG_POOL"))
+    std::fprintf(stderr, "nkhip pool %p (%lld vectors of %lld B, %s)\n", static_cast<void*>(pool_),
+                 static_cast<long long>(count), static_cast<long long>(sizeof(double) * npad),
+                 vmm_base_ ? "chunk-mapped" : (external ? "external" : "hipMalloc"));
+  out->resize(count);
+  for (int i = 0; i < count; ++i) (*out)[i] = pool_ + npad * i;
+  pool_count_ = count;
   return NK_OK;
 }
 
@@ -491,6 +582,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
   st_ = st ? st : &dummy;
   std::memset(st_, 0, sizeof(nk_stats));
   st_->step_min = 1.0;
+  steps_.clear();
   ocount_ = 0;
   ohead_ = 0;
   const int64_t n = E_.n;
@@ -546,6 +638,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
     if (rc) break;
     if (s != 1.0) st_->n_backtrack += 1;
     st_->step_min = std::min(st_->step_min, s);
+    steps_.push_back(s);
     std::swap(X_, Xt_);
     std::swap(Fx_, Ft_);
     std::swap(G0_, Gt_);

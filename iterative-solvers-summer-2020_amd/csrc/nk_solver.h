@@ -71,8 +71,10 @@ class Engine {
 
   // Allocate `count` zeroed vectors of npad doubles from one pool (or carve from `external`).
   // With enable_edges() called first, every pool vector also gets an edge array (edges()).
+  // Pools of >= 256 MB are mapped in chunks through the virtual memory API (vmm_alloc).
   int alloc(int count, std::vector<double*>* out, void* external = nullptr,
             int64_t external_bytes = 0);
+  bool pool_chunk_mapped() const { return vmm_base_ != nullptr; }
   // Edge arrays (nk_kernels.h, kEdgeW) of an ny x nx grid for the pool vectors.
   void enable_edges(int64_t ny, int64_t nx) {
     edge_ny_ = ny;
@@ -159,6 +161,12 @@ class Engine {
   double* dres_ = nullptr;
   double* hres_ = nullptr;
   int64_t bytes_ = 0;
+  // a pool mapped through the virtual memory API (vmm_alloc): reserved range and its handles
+  void* vmm_base_ = nullptr;
+  size_t vmm_size_ = 0, vmm_chunk_ = 0;
+  std::vector<hipMemGenericAllocationHandle_t> vmm_h_;
+  int vmm_alloc(size_t bytes, size_t chunk);
+  void vmm_free();
   struct Pending {
     int kind;
     hipEvent_t a, b;
@@ -250,6 +258,9 @@ class NewtonKrylov {
   // x_out = root of F starting from x_in (device, length n; may alias).  Returns NK_* status.
   int solve(const double* x_in, double* x_out, nk_stats* st);
   static int vectors_needed(const nk_opts& o) { return o.inner_m + 2 * o.outer_k + 8; }
+  // Accepted Armijo step s of every Newton iteration of the last solve (scipy's
+  // scalar_search_armijo result, _nonlin.py:294-314; 1 where no line search ran).
+  const std::vector<double>& step_log() const { return steps_; }
 
  private:
   int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
@@ -282,6 +293,7 @@ class NewtonKrylov {
   double omega_ = 0.0;
   double* d_ = nullptr;  // current search direction (an outer slot)
   nk_stats* st_ = nullptr;
+  std::vector<double> steps_;  // step_log()
   double fx_norm_ = 0.0;
   double rdiff_ = 0.0;
 };

@@ -167,14 +167,24 @@ __device__ __forceinline__ double2 ld_p0(const StencilArgs& A, const double* p) 
 template <SMode M>
 constexpr int kFields = (kComb<M> || kTwo<M>) ? 2 : 1;
 
+// Grid: gx column blocks x gy bands, launched as one dimension rounded up to a multiple of 8 and
+// mapped XCD-aware: the hardware deals consecutive workgroups round-robin over the 8 XCDs, so
+// logical block L = (b % 8) (blocks / 8) + b / 8 gives each XCD one contiguous run of whole
+// bands.  The two neighbouring column blocks of a band (whose edge lines a block's c-2 / c+2 side
+// loads touch) and the neighbouring bands (whose halo rows it re-reads) then share one L2: with
+// the plain mapping adjacent column blocks sat on different XCDs and every block edge line was
+// fetched from HBM twice (FD JVP traffic 1.107x algorithmic, profiles/r02f_traffic.json).
 template <SMode M, int BX, int PF>
-__global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
+__global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx, int gy) {
   constexpr int R = kRad<M>;
   constexpr int NR = 2 * R + 1;
   constexpr int RING = NR + PF;
   constexpr int NF = kFields<M>;
   const int64_t nx = A.nx, ny = A.ny;
-  const int64_t c0 = 2 * (int64_t(blockIdx.x) * BX + threadIdx.x);
+  const int64_t lb = (int64_t(blockIdx.x) % 8) * (int64_t(gridDim.x) / 8) + blockIdx.x / 8;
+  if (lb >= int64_t(gx) * gy) return;  // padding of the grid to a multiple of 8
+  const int64_t bx = lb % gx, by = lb / gx;
+  const int64_t c0 = 2 * (bx * BX + threadIdx.x);
   const bool active = c0 < nx;
   const int64_t cc = active ? c0 : 0;
   const int64_t cm = (cc >= 2) ? cc - 2 : cc - 2 + nx;
@@ -213,7 +223,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   // in L2.  The window sums pair the rows symmetrically about the centre, so the result is
   // bitwise the same in either direction (fp addition is commutative).
   // A.rev walks the bands from the top of the grid (see traversal_reverse)
-  const int64_t band = A.rev ? int64_t(gridDim.y) - 1 - blockIdx.y : int64_t(blockIdx.y);
+  const int64_t band = A.rev ? int64_t(gy) - 1 - by : by;
   const int64_t r0 = band * RY;
   const int64_t r1 = (r0 + RY < ny) ? r0 + RY : ny;
   const bool up = (band & 1) != 0;
@@ -291,8 +301,8 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY) {
   }
   if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
-    const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
-    const int64_t bid = band * gridDim.x + blockIdx.x;  // slot by band: independent of A.rev
+    const int64_t nblk = int64_t(gx) * gy;
+    const int64_t bid = band * gx + bx;  // slot by band: independent of A.rev
     if (threadIdx.x < 3) A.partial[threadIdx.x * nblk + bid] = v;
   }
 }
@@ -399,16 +409,16 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     if (k > 6) k = 6;
     const int RY = int(k * ring);
     const int64_t gy = (A.ny + RY - 1) / RY;
-    if (gy > 65535) return hipErrorInvalidValue;
+    if (gx * gy > (int64_t(1) << 31) - 8) return hipErrorInvalidValue;
     if (nblk) *nblk = gx * gy;
     B.rev = traversal_reverse();
     static const bool nt_p0 = env_int("NKHIP_NT_P0", 1) != 0;
     B.nt_p0 = nt_p0;
-    const dim3 grid{unsigned(gx), unsigned(gy), 1u};
+    const dim3 grid{unsigned((gx * gy + 7) / 8 * 8), 1u, 1u};
     if (pf == 2)
-      hipLaunchKernelGGL((march_kernel<M, BX, 2>), grid, dim3(BX), 0, s, B, RY);
+      hipLaunchKernelGGL((march_kernel<M, BX, 2>), grid, dim3(BX), 0, s, B, RY, int(gx), int(gy));
     else
-      hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY);
+      hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY, int(gx), int(gy));
   } else {
     const int64_t n = A.nx * A.ny;
     const int64_t g = (n + 255) / 256;

@@ -10,7 +10,7 @@ from ._lib import NKError, lib, status_string  # noqa: F401
 from .dist import RcclComm, loopback_comms, neighbours, slab_rows  # noqa: F401
 from .droplet import Droplet, read_init, write_init  # noqa: F401
 from .mems import Mems  # noqa: F401
-from .ops import (axpy, dot, lap5_apply, maxnorm, maxpy, mdot, nrm2, scal, sh13_apply,  # noqa: F401
+from .ops import (axpy, dot, lap5_apply, maxnorm, maxpy, mdot, nrm2, scal, sh13_apply, stream_copy,  # noqa: F401
                   sh_arnoldi_fused, edge_gather, arnoldi_mbox_launches, sh_fdjvp, sh_jvp, sh_residual)
 from .sh import SwiftHohenberg, sh_step  # noqa: F401
 from .shlin import SHLinearised  # noqa: F401

@@ -21,6 +21,7 @@ NK_EINVAL = -1
 NK_EHIP = -2
 NK_ECOMM = -3
 NK_ENOMEM = -4
+ABI_VERSION = 3  # include/nkhip.h NKHIP_ABI_VERSION: the struct layouts below
 NK_JVP_FD = 0
 NK_JVP_ANALYTIC = 1
 
@@ -73,6 +74,7 @@ _I32 = C.c_int32
 # (name, restype, argtypes) -- exactly the entry points of include/nkhip.h
 SIGNATURES = [
     ("nk_version", C.c_char_p, []),
+    ("nk_abi_version", C.c_int, []),
     ("nk_opts_default", C.c_int, [C.POINTER(nk_opts)]),
     ("nk_status_string", C.c_char_p, [C.c_int]),
     ("nk_lap5_apply", C.c_int, [_P, _P, _I64, _I64, _D, _P]),
@@ -96,6 +98,7 @@ SIGNATURES = [
     ("nk_scal", C.c_int, [_D, _P, _I64, _P]),
     ("nk_mdot", C.c_int, [C.POINTER(_P), _I32, _P, _I64, C.POINTER(_D), _P]),
     ("nk_maxpy", C.c_int, [C.POINTER(_P), C.POINTER(_D), _I32, _P, _I64, _P]),
+    ("nk_stream_copy", C.c_int, [_P, _P, _I64, _P]),
     ("nk_comm_unique_id_bytes", C.c_int, []),
     ("nk_comm_get_unique_id", C.c_int, [_P]),
     ("nk_comm_create_rccl", C.c_int, [C.POINTER(_P), _P, _I32, _I32]),
@@ -109,6 +112,7 @@ SIGNATURES = [
     ("nk_sh_set_opts", C.c_int, [_P, C.POINTER(nk_opts)]),
     ("nk_sh_kernel_profile", C.c_int, [_P, C.POINTER(nk_kprof), _I32]),
     ("nk_sh_reset_profile", C.c_int, [_P]),
+    ("nk_sh_step_log", C.c_int, [_P, C.POINTER(_D), _I32]),
     ("nk_sh_workspace_bytes", C.c_int64, [_P]),
     ("nk_solve_workspace_bytes", C.c_int64, [_I64, C.POINTER(nk_opts)]),
     ("nk_solve", C.c_int, [RESIDUAL_FN, _P, _P, _P, _I64, C.POINTER(nk_opts),
@@ -154,6 +158,10 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    got = lib.nk_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError(f"nkhip: {path} has C-ABI version {got}, this binding expects "
+                          f"{ABI_VERSION} (rebuild the library)")
     return lib
 
 

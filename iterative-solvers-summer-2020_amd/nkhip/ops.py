@@ -204,3 +204,14 @@ def maxpy(V, coef, y):
     cs = (C.c_double * max(m, 1))(*[float(c) for c in coef])
     check(lib.nk_maxpy(ptrs, cs, m, _ptr(y), y.numel(), _stream()), "nk_maxpy")
     return y
+
+
+def stream_copy(src, out=None):
+    """out = src through nk_stream_copy (16-KB chunks per block, non-temporal): the bench's probe
+    of the box's achievable streaming rate."""
+    src = _dev(src, "src")
+    out = torch.empty_like(src) if out is None else _dev(out, "out")
+    if out.numel() != src.numel():
+        raise ValueError("stream_copy: size mismatch")
+    check(lib.nk_stream_copy(_ptr(src), _ptr(out), src.numel(), _stream()), "nk_stream_copy")
+    return out

@@ -154,6 +154,14 @@ class SwiftHohenberg:
     def workspace_bytes(self) -> int:
         return int(lib.nk_sh_workspace_bytes(self._h))
 
+    def step_log(self):
+        """The accepted Armijo step of every Newton iteration of the last step (the ``step %g``
+        column of the reference's verbose output, sh_scipy_nk.py:61)."""
+        n = check(lib.nk_sh_step_log(self._h, None, 0), "nk_sh_step_log")
+        buf = (C.c_double * max(n, 1))()
+        check(lib.nk_sh_step_log(self._h, buf, n), "nk_sh_step_log")
+        return [buf[i] for i in range(n)]
+
 
 def sh_step(U, h, k=0.2, r=0.01, g=1.0, **kw):
     """Functional form: the next implicit step of a 2-D periodic grid with mesh spacing h."""

@@ -52,6 +52,7 @@ def test_python_binding_matches_header():
 def test_host_only_helpers():
     import nkhip._lib as L
     assert L.lib.nk_version().decode().startswith("nkhip")
+    assert L.lib.nk_abi_version() == L.ABI_VERSION == 3
     o = L.default_opts()
     assert o.inner_m == 30 and o.outer_k == 10 and o.line_search == 1
     assert math.isnan(o.f_tol) and o.jvp_mode == L.NK_JVP_FD and o.maxiter == 0

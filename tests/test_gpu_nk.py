@@ -77,6 +77,34 @@ def test_sh_step_fevals_match_scipy(name, fused, monkeypatch):
     m.close()
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_line_search_steps_match_scipy(fused, monkeypatch):
+    """SURVEY 8a row A9, step by step: the accepted Armijo step of EVERY Newton iteration of the
+    reference's backtracking step (the `step %g` column of its verbose line, sh_scipy_nk.py:61 ->
+    scipy/optimize/_linesearch.py:684-739) against the fixture's sequence, within 2 %, with the
+    same backtracking pattern, on both the unfused path (SciPy's two-evaluation FD quotient,
+    MGS-equivalent Gram solve) and the fused one (closed-form quotient).  F calls are NOT exact:
+    with eta ~ 0.9 every LGMRES call stops on a residual test that FD rounding noise moves by a
+    step either way -- the NumPy restatement of SciPy itself is 3 % off on this fixture
+    (test_oracle.py), the GPU measured 209 vs 217 (unfused) -- so the count is held to 5 %."""
+    monkeypatch.setenv("NKHIP_FUSED", fused)
+    z = load_golden("nk_n61_amp3_backtrack")
+    m, _ = _model(z, jvp="fd")
+    N = int(z["N"])
+    m.step(torch.as_tensor(z["traj"][0].reshape(N, N), device="cuda"))
+    st, got = m.last_stats, np.array(m.step_log())
+    m.close()
+    ref = z["steps"]
+    assert st["status"] == 0
+    assert len(got) == len(ref), (got, ref)
+    np.testing.assert_array_equal(got < 1, ref < 1)
+    assert np.all(np.abs(got - ref) <= 0.02 * ref), np.c_[got, ref]
+    ref_f = int(z["nfev"][0])
+    assert abs(st["nfev"] + st["njvp"] - ref_f) <= 0.05 * ref_f, (st, ref_f)
+    print(f"fused={fused}: steps max rel diff {float(np.max(np.abs(got - ref) / ref)):.2e}, "
+          f"F calls {st['nfev'] + st['njvp']} (scipy {ref_f})")
+
+
 def test_line_search_backtracks_like_scipy():
     """SURVEY 8a row A9 on the GPU: the reference's Newton step from a large-amplitude start
     backtracks in 5 of its 13 iterations (quadratic and cubic branches of scalar_search_armijo).
@@ -227,6 +255,66 @@ def test_config4_4096_step():
         assert np.abs(F).max() <= 1.01 * np.finfo(float).eps ** (1 / 3), (fused, np.abs(F).max())
     scale = max(1.0, float(np.abs(out["0"]).max()))
     assert float(np.abs(out["1"] - out["0"]).max()) <= 1e-5 * scale
+
+
+def test_config4_matches_reference_step():
+    """Config 4 pinned to the reference itself: scipy's newton_krylov on the reference's own
+    4096^2 CSR residual (sh_scipy_nk.py:1-49 with N = 4096, d = 2560; tests/golden/
+    make_golden_config4.py) from default_rng(2020), one step at the default f_tol.  The fixture
+    holds 64 strided rows of the result and every row's sum: the GPU step (fused kernel, the
+    bench path) must match the rows to 1e-5 max(1, |U|) (SURVEY 7 hard part 1, default f_tol),
+    every row sum to the same bound times nx, and the Newton count to +-1."""
+    import nkhip
+    z = load_golden("nk_n4096_h0625_sampled")
+    N = int(z["N"])
+    U0 = np.random.default_rng(int(z["seed"])).standard_normal((N, N))
+    m = nkhip.SwiftHohenberg(N=N, d=float(z["d"]), k=float(z["k"]), r=float(z["r"]),
+                             g=float(z["g"]))
+    U1 = m.step(torch.as_tensor(U0, device="cuda"))
+    st = dict(m.last_stats)
+    m.close()
+    assert st["status"] == 0
+    assert abs(st["nit"] - int(z["nit"][0])) <= 1, (st, z["nit"])
+    scale = max(1.0, float(z["U1_absmax"]))
+    rows = U1[torch.as_tensor(z["rows"], device="cuda")].cpu().numpy()
+    err = float(np.abs(rows - z["U1_rows"]).max())
+    assert err <= 1e-5 * scale, err
+    sums = U1.sum(dim=1).cpu().numpy()
+    assert float(np.abs(sums - z["U1_rowsum"]).max()) <= 1e-5 * scale * N
+    assert abs(float(U1.abs().max()) - float(z["U1_absmax"])) <= 1e-5 * scale
+    print(f"config 4 vs reference: rows {err:.2e}, row sums "
+          f"{float(np.abs(sums - z['U1_rowsum']).max()):.2e}, nit {st['nit']} "
+          f"(scipy {int(z['nit'][0])}), F+JVP {st['nfev'] + st['njvp']} (scipy {int(z['nfev'][0])})")
+
+
+def test_trajectory_100_steps_matches_reference():
+    """The time loop itself (sh_scipy_nk.py:53-61) at the reference defaults (N = 64, d = 40):
+    100 consecutive GPU steps from default_rng(2020) against the reference's 100 scipy steps,
+    compared at every 10th step.  Each step is solved to the default f_tol, so the two
+    trajectories differ by solver rounding only: the bound is the per-step one of SURVEY 7 hard
+    part 1 (1e-5 max(1, |U|)), required at every 10th step -- drift over the loop stays inside
+    it.  Newton counts: within +-1 per step, and the 100-step total within 2 %."""
+    import nkhip
+    z = load_golden("nk_n64_traj100")
+    N = int(z["N"])
+    m = nkhip.SwiftHohenberg(N=N, d=float(z["d"]), k=float(z["k"]), r=float(z["r"]),
+                             g=float(z["g"]))
+    U = torch.as_tensor(z["traj"][0].reshape(N, N), device="cuda")
+    nits, errs = [], []
+    for s in range(1, int(z["steps"][-1]) + 1):
+        U = m.step(U)
+        assert m.last_stats["status"] == 0
+        nits.append(m.last_stats["nit"])
+        if s % 10 == 0:
+            ref = z["traj"][s // 10]
+            errs.append(float(np.abs(U.cpu().numpy().reshape(-1) - ref).max()))
+            assert errs[-1] <= 1e-5 * max(1.0, float(np.abs(ref).max())), (s, errs)
+    m.close()
+    ref_nit = z["nit"].astype(int)
+    assert np.all(np.abs(np.array(nits) - ref_nit) <= 1), np.c_[nits, ref_nit]
+    assert abs(sum(nits) - ref_nit.sum()) <= 0.02 * ref_nit.sum()
+    print("trajectory max|dU| at steps 10..100:", ["%.1e" % e for e in errs], "nit", sum(nits),
+          "scipy", int(ref_nit.sum()))
 
 
 def _residual_rows(U1, U0, h, r, k, g, chunk=2048):
