@@ -185,11 +185,14 @@ int nk_comm_create_rccl(nk_comm** out, const void* unique_id, int32_t rank, int3
  * logic on a single GPU): fills out[0..nranks-1]. */
 int nk_comm_create_loopback(nk_comm** out, int32_t nranks);
 int nk_comm_destroy(nk_comm* c);
-/* Marks the group failed: every rank blocked in, or later entering, a collective of this group
- * returns NK_ECOMM instead of waiting for the failed rank (loopback: wakes the waiting threads;
- * RCCL: the communicator is aborted with ncclCommAbort at destroy).  A stepper calls it itself
- * when one of its steps fails with a negative code; a host thread that fails outside the
- * library calls it before it exits. */
+/* Marks the group failed.  Loopback (one process): every rank blocked in, or later entering, a
+ * collective of the group returns NK_ECOMM instead of waiting for the failed rank (the waiting
+ * threads are woken).  RCCL (one process per GPU): this rank's communicator is aborted at once
+ * (ncclCommAbort) and its later calls return NK_ECOMM; peer processes are NOT notified -- a peer
+ * blocked in a collective with the failed rank is released by the launcher's own failure
+ * handling (e.g. the torch.distributed watchdog), so that guarantee is the loopback group's
+ * only.  A stepper calls it itself when one of its steps fails with a negative code; a host
+ * thread that fails outside the library calls it before it exits. */
 int nk_comm_abort(nk_comm* c);
 
 /* ---------------- Swift-Hohenberg implicit time step (the north-star path) ---------------- */

@@ -7,6 +7,7 @@
 #include <mutex>
 #include <memory>
 #include <new>
+#include <vector>
 
 #include "../../include/nkhip.h"
 #include "comm.h"
@@ -163,10 +164,13 @@ int attach_mbox(ArnoldiArgs& A) {
   static double* buf = nullptr;
   static int64_t cap = 0;
   static uint64_t tag = 0;
+  // grow-only: a buffer once handed out is never freed (another thread may be about to launch
+  // with it after this lock is released); the outgrown ones are kept until process exit
+  static std::vector<double*> retired;
   std::lock_guard<std::mutex> lk(mu);
   const int64_t need = arnoldi_mbox_elems(A.ny, A.nx);
   if (cap < need) {
-    if (buf) hipFree(buf);
+    if (buf) retired.push_back(buf);
     buf = nullptr;
     cap = 0;
     if (hipMalloc(reinterpret_cast<void**>(&buf), sizeof(double) * need) != hipSuccess)

@@ -25,18 +25,14 @@ struct RcclComm final : nk_comm {
   double* bar = nullptr;  // barrier scratch, allocated on first use
   bool aborted = false;
   ~RcclComm() override {
-    if (c) {
-      if (aborted)
-        ncclCommAbort(c);
-      else
-        ncclCommDestroy(c);
-    }
+    if (c) ncclCommDestroy(c);  // an aborted communicator was released in abort()
     if (bar) hipFree(bar);
   }
   int rank() const override { return r; }
   int size() const override { return p; }
 
   int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
+    if (aborted) return NK_ECOMM;
     if (nsum > 0 && ncclAllReduce(dev, dev, size_t(nsum), ncclDouble, ncclSum, c, s) != ncclSuccess)
       return NK_ECOMM;
     if (nv > nsum &&
@@ -79,7 +75,18 @@ struct RcclComm final : nk_comm {
     return hipStreamSynchronize(s) == hipSuccess ? NK_OK : NK_EHIP;
   }
 
-  void abort() override { aborted = true; }
+  // Aborts this rank's communicator at once (ncclCommAbort releases its enqueued RCCL work and
+  // its resources); every later call of this rank returns NK_ECOMM.  Peer PROCESSES are not
+  // told: a peer blocked in a collective with this rank is released by its own failure handling
+  // (the launcher / torch.distributed watchdog), not by this call (nkhip.h nk_comm_abort).
+  void abort() override {
+    if (aborted) return;
+    aborted = true;
+    if (c) {
+      ncclCommAbort(c);
+      c = nullptr;
+    }
+  }
 };
 
 // ------------------------------------------------------------------------------------------

@@ -464,9 +464,16 @@ int NewtonKrylov::device_steps() {
     V_[u + 1] = rot[u].v;
     ++voided;
   }
-  // ... and their launches did no work: out of the kernel profile
+  // ... and their launches did no work: out of the kernel profile (the fused launches, and the
+  // reduction + control launches each of those steps queued behind it)
   P_.void_fused_steps(voided);
+  E_.void_last(K_CTL, voided);
+  if (!one) E_.void_last(K_REDUCE, voided);
   if (rc) return rc;
+  // The voided reduction of slot_mdot(t + 1) may still write that pinned host slot after the
+  // host resumes; drain the stream here so no later poll of the slot can meet a stale write
+  // (one synchronisation per hand-back, i.e. per LGMRES call).
+  if (voided > 0 && (rc = E_.sync()) != NK_OK) return rc;
   if (S.j != t || S.halt != 1 + t) return NK_EHIP;
   S.halt = 0;
   return NK_OK;
