@@ -129,3 +129,23 @@ def test_nk_restatement_backtracks_like_scipy():
     np.testing.assert_allclose(st.steps, ref, rtol=3e-2)
     assert abs(st.nfev - int(z["nfev"][0])) <= 0.03 * int(z["nfev"][0])
     assert np.abs(u - z["traj"][1]).max() <= 1e-5 * max(1.0, np.abs(z["traj"][1]).max())
+
+
+def test_nk_restatement_tracks_reference_trajectory():
+    """The time loop (sh_scipy_nk.py:53-61) at the reference defaults (N = 64, d = 40): the
+    NumPy restatement of SciPy's newton_krylov, stepped 100 times from default_rng(2020), stays
+    within 1e-7 of the reference's own trajectory at every 10th step (measured 9e-9 at step 100)
+    with the same Newton count per step.  Pins tests/golden/nk_n64_traj100.npz."""
+    z = load_golden("nk_n64_traj100")
+    N, h, r, k, g = int(z["N"]), float(z["h"]), float(z["r"]), float(z["k"]), float(z["g"])
+    U = z["traj"][0].copy()
+    nits = []
+    for s in range(1, int(z["steps"][-1]) + 1):
+        uo = U.copy()
+        F = lambda u: sh_oracle.residual(u, uo, N, N, h, r, k, g)  # noqa: E731
+        U, st = nk_oracle.newton_krylov(F, uo, return_stats=True, ortho="mgs")
+        nits.append(st.nit)
+        if s % 10 == 0:
+            ref = z["traj"][s // 10]
+            assert np.abs(U - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max()), s
+    assert nits == [int(x) for x in z["nit"]]
