@@ -39,29 +39,13 @@
 namespace nk {
 namespace {
 
-#ifndef ARN_DPPHALO
-#define ARN_DPPHALO 1
-#endif
-#ifndef ARN_SELECT
-#define ARN_SELECT 1
-#endif
-#ifndef ARN_DPPNB
-#define ARN_DPPNB 1
-#endif
-
-#ifndef ARN_WPB
-#define ARN_WPB 4
-#endif
-constexpr int kSW = 64;       // columns per wave (one per lane)
-constexpr int WPB = ARN_WPB;  // waves per block (the packed halo loads carry 16 * WPB entries)
+constexpr int kSW = 64;  // columns per wave (one per lane)
+constexpr int WPB = 4;   // waves per block (the packed halo loads carry 16 * WPB entries)
 static_assert(WPB * kSW == kEdgeW, "edge arrays are laid out for the fused kernel's blocks");
 // waves per block of the mailbox instantiation: it reads no edge arrays, and its halos cost a
 // record per block side, so narrower blocks (less LDS lag per block, 2-wave barriers) pay:
 // nv 24 0.602-0.610 -> 0.618-0.619 of 8 TB/s with 2 waves (profiles/r02_arnoldi_ab.md)
-#ifndef ARN_MBWPB
-#define ARN_MBWPB 2
-#endif
-constexpr int kMbWPB = ARN_MBWPB;
+constexpr int kMbWPB = 2;
 
 __device__ __forceinline__ double applyL13(const SHCoef& k, double c, double a1, double dg,
                                            double a2) {
@@ -82,13 +66,7 @@ __device__ __forceinline__ double ldb(const double* base, uint32_t off) {
 // arguments loses its address space in inference and becomes a flat load, whose wait the
 // compiler widens to vmcnt(0) -- draining the whole row's load batch once per row.
 typedef const double __attribute__((address_space(1))) gdouble;
-#ifndef ARN_FLAT
-#define ARN_FLAT 0
-#endif
-__device__ __forceinline__ double gld(const double* p) {
-  if constexpr (ARN_FLAT) return *p;  // A/B only: the round-2 flat loads
-  return *(gdouble*)p;
-}
+__device__ __forceinline__ double gld(const double* p) { return *(gdouble*)p; }
 
 // Stores through a raw buffer resource: a lane whose offset is out of range (kOOB) writes
 // nothing, so masked stores need no branch.
@@ -175,11 +153,6 @@ typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef const dv2 __attribute__((address_space(1))) gdv2;
 template <bool NT>
 __device__ __forceinline__ dv2 gld2(const double* a) {
-  if constexpr (ARN_FLAT) {
-    const dv2* f = reinterpret_cast<const dv2*>(a);
-    if constexpr (NT) return __builtin_nontemporal_load(f);
-    return *f;
-  }
   gdv2* p = (gdv2*)a;
   if constexpr (NT) return __builtin_nontemporal_load(p);
   return *p;
@@ -204,10 +177,9 @@ __device__ __forceinline__ dv2 gld2(const double* a) {
 // XCD -- is waited for a bounded number of polls, after which the lane recomputes the pair
 // itself, in the producer's exact summation order (same result bits), and stops polling for
 // the rest of the launch: correctness never depends on co-residency.
-#ifndef ARN_MB_AUX
-#define ARN_MB_AUX 16
-#endif
-constexpr uint32_t kMBCoh = ARN_MB_AUX;  // cache policy of the record loads / stores (16: sc1)
+// cache policy of the record loads / stores: sc1 (device scope; sc0 records were never visible
+// in time, profiles/r02_arnoldi_ab.md)
+constexpr uint32_t kMBCoh = 16;
 constexpr int kMBSpin = 2048;     // polls before a lane recomputes a missing halo pair itself
 __device__ __forceinline__ uint32_t mb_off(int64_t blk, int64_t T, int64_t t, int side, int comp) {
   return uint32_t((((blk * T + t) * 4) + side * 2 + comp) * 16);
@@ -534,19 +506,11 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       // of each 16-lane row (DPP row shifts), then the rows in pairs (permlane16/32 swaps);
       // lanes 12..15 end with the totals
       double hs = hcf * s.hv;
-#if ARN_DPPHALO
       hs += dpp_row_shr(hs, 4);
       hs += dpp_row_shr(hs, 8);
       hs = pair16_sum(hs);
       hs = pair_sum(hs);
       if ((lane & ~3) == 12) hpart[slot][wid][lane & 3] = hs;
-#else
-      hs += __shfl_xor(hs, 4, 64);
-      hs += __shfl_xor(hs, 8, 64);
-      hs += __shfl_xor(hs, 16, 64);
-      hs += __shfl_xor(hs, 32, 64);
-      if (lane < 4) hpart[slot][wid][lane] = hs;
-#endif
     }
     if (lane == 0) {
       edge[slot][wid][0] = u.x;
@@ -570,7 +534,6 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     // lanes 0..3: block halo columns -2, -1, +0, +1
     const double yh = s.own ? hz : s.hx;  // u on the halo columns
     const int wl = (wid > 0) ? wid - 1 : 0, wr = (wid < WB - 1) ? wid + 1 : WB - 1;
-#if ARN_SELECT
     // both candidates are read unconditionally (a uniform select, no branch around LDS reads)
     const double el2 = edge[slot][wl][2], el1 = edge[slot][wl][3];
     const double er1 = edge[slot][wr][0], er2 = edge[slot][wr][1];
@@ -578,21 +541,10 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const double hr1 = readlane(yh, 2), hr2 = readlane(yh, 3);
     const double yl2 = (wid == 0) ? hl2 : el2, yl1 = (wid == 0) ? hl1 : el1;
     const double yr1 = (wid == WB - 1) ? hr1 : er1, yr2 = (wid == WB - 1) ? hr2 : er2;
-#else
-    const double yl2 = (wid == 0) ? readlane(yh, 0) : edge[slot][wl][2];
-    const double yl1 = (wid == 0) ? readlane(yh, 1) : edge[slot][wl][3];
-    const double yr1 = (wid == WB - 1) ? readlane(yh, 2) : edge[slot][wr][0];
-    const double yr2 = (wid == WB - 1) ? readlane(yh, 3) : edge[slot][wr][1];
-#endif
     // neighbours inside the half: lane l-1 holds columns 2l-2, 2l-1 (the lanes whose neighbour
     // is across the half boundary take the edge values below)
-#if ARN_DPPNB
     const double ux = dpp_up(u.x), uy = dpp_up(u.y);
     const double dx = dpp_down(u.x), dy = dpp_down(u.y);
-#else
-    const double ux = __shfl_up(u.x, 1, 32), uy = __shfl_up(u.y, 1, 32);
-    const double dx = __shfl_down(u.x, 1, 32), dy = __shfl_down(u.y, 1, 32);
-#endif
     const double cm2 = (l == 0) ? yl2 : ux, cm1 = (l == 0) ? yl1 : uy;   // columns 2l-2, 2l-1
     const double cp2 = (l == 31) ? yr1 : dx, cp3 = (l == 31) ? yr2 : dy;  // columns 2l+2, 2l+3
 #pragma unroll
@@ -1248,25 +1200,15 @@ hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   return launch_grid<NV>(kern, occ, WPB, kern_mb, occ_mb, WM, !EXT, kSW, A, s, nwaves);
 }
 
-#ifndef ARN_WIDEW
-#define ARN_WIDEW 4
-#endif
-#ifndef ARN_WIDE_MB
-#define ARN_WIDE_MB 0
-#endif
-constexpr int kWideW = ARN_WIDEW;  // waves per block of the wide layout (512 columns)
+constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
 template <int NV, bool EXT, int PF, bool NT>
 hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   // no mailbox instantiation: with 512-column blocks the packed halo is the cheaper one
   // (4096^2, one box: n4 0.63 vs 0.55, n12 0.64 vs 0.63, n18 0.62 vs 0.57 of 8 TB/s)
+  // (the wide kernel keeps a mailbox instantiation parameter, MB; it measured no gain with 2- or
+  // 4-wave blocks, profiles/r02_arnoldi_ab.md, and is not instantiated)
   auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW, false>;
   static const Occ occ = query_occ(kern, 64 * kWideW);
-  if constexpr (ARN_WIDE_MB != 0) {  // experiment: a mailbox instantiation for the wide layout
-    constexpr int WM = ARN_WIDE_MB;
-    auto kern_mb = arnoldi_wide_kernel<NV, EXT, PF, NT, WM, !EXT>;
-    static const Occ occ_mb = query_occ(kern_mb, 64 * WM);
-    return launch_grid<NV>(kern, occ, kWideW, kern_mb, occ_mb, WM, !EXT, kWW, A, s, nwaves);
-  }
   return launch_grid<NV>(kern, occ, kWideW, kern, occ, kWideW, false, kWW, A, s, nwaves);
 }
 
