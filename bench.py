@@ -39,8 +39,13 @@ def parse():
     ap.add_argument("--n", type=int, default=4096, help="grid points per side")
     ap.add_argument("--jvp", choices=["fd", "analytic"], default="fd")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--comm", choices=["peer", "rccl"], default="peer",
+                    help="slab communicator for N > 1: peer-memory kernels over xGMI (default) "
+                         "or RCCL send/recv + all-reduce")
     ap.add_argument("--rccl-self", action="store_true",
                     help="testing: build the RCCL communicator even at world size 1")
+    ap.add_argument("--peer-self", action="store_true",
+                    help="testing: build the peer-memory communicator even at world size 1")
     ap.add_argument("--extra", choices=["on", "off"], default="on",
                     help="also measure configs 2 (1024^2 Lap SpMV) and 3 (91x61 droplet)")
     return ap.parse_args()
@@ -344,14 +349,18 @@ def main():
             sys.exit(2)
     torch.cuda.set_device(local)
     comm = None
-    if world > 1 or args.rccl_self:
+    use_dist = world > 1 or args.rccl_self or args.peer_self
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if world == 1:  # --rccl-self without a launcher: a world of one
+        if world == 1:  # --rccl-self / --peer-self without a launcher: a world of one
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
             os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        comm = nkhip.RcclComm.from_torch_distributed()
+        if args.rccl_self or (world > 1 and args.comm == "rccl" and not args.peer_self):
+            comm = nkhip.RcclComm.from_torch_distributed()
+        else:
+            comm = nkhip.PeerComm.from_torch_distributed(max_nx=args.n)
 
     n = args.n
     h, k, r, g = 0.625, 0.2, 0.01, 1.0
@@ -368,7 +377,7 @@ def main():
     a, b = U, torch.empty_like(U)
 
     def barrier():
-        if world > 1 or args.rccl_self:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -461,7 +470,8 @@ def main():
             "config": {"workload": f"swift_hohenberg_cn_newton_krylov_{n}x{n}", "grid": [n, n],
                        "h": h, "k": k, "r": r, "g": g, "jvp": args.jvp,
                        "f_tol": "scipy default eps^(1/3) (max-norm)", "inner_m": 30,
-                       "outer_k": 10, "parallelism": f"row-slab x{world} (RCCL halo)"},
+                       "outer_k": 10, "parallelism": f"row-slab x{world}",
+                       "comm": (type(comm).__name__ if comm is not None else "none")},
             "newton_its_per_s": round(tot["nit"] / elapsed, 3),
             "jvps_per_s": round(tot["njvp"] / elapsed, 2),
             "per_step": {k_: v / args.steps for k_, v in tot.items()},
@@ -509,10 +519,12 @@ def main():
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),
                                     "droplet_init": config_droplet_init()}
         print(json.dumps(out), flush=True)
+    if use_dist:
+        dist.barrier()  # no rank frees its communicator buffers while a peer may still use them
     model.close()
     if comm is not None:
         comm.close()
-    if world > 1 or args.rccl_self:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -370,6 +370,12 @@ int nk_comm_create_rccl(nk_comm** out, const void* uid, int32_t rank, int32_t nr
 int nk_comm_create_loopback(nk_comm** out, int32_t nranks) {
   return comm_create_loopback(out, nranks);
 }
+int nk_comm_peer_handle_bytes(void) { return comm_peer_handle_bytes(); }
+int nk_comm_create_peer(nk_comm** out, int32_t rank, int32_t nranks, int64_t max_nx,
+                        void* handle_out) {
+  return comm_create_peer(out, rank, nranks, max_nx, handle_out);
+}
+int nk_comm_peer_connect(nk_comm* c, const void* handles) { return comm_peer_connect(c, handles); }
 int nk_comm_destroy(nk_comm* c) {
   delete c;
   return NK_OK;

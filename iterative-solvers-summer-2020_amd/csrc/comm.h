@@ -30,6 +30,9 @@ struct nk_comm {
   // the ranks' kernels share one device (loopback): launches of different ranks run
   // concurrently, so a kernel cannot count on its whole grid being resident
   virtual bool shares_device() const { return false; }
+  // a collective already enqueued on the device failed (peer-memory communicator: a wait timed
+  // out or the group was aborted); checked after each stream synchronisation (Engine::sync)
+  virtual bool failed() const { return false; }
 };
 
 namespace nk {
@@ -37,4 +40,9 @@ int comm_unique_id_bytes();
 int comm_get_unique_id(void* out);
 int comm_create_rccl(nk_comm** out, const void* uid, int rank, int nranks);
 int comm_create_loopback(nk_comm** out, int nranks);
+// peer-memory communicator (peer.hip): create (allocate + export this rank's buffer, write its
+// handle blob), then connect with every rank's blob (rank order)
+int comm_peer_handle_bytes();
+int comm_create_peer(nk_comm** out, int rank, int nranks, int64_t max_nx, void* handle_out);
+int comm_peer_connect(nk_comm* c, const void* handles);
 }  // namespace nk

@@ -287,7 +287,8 @@ void Engine::reset_stats() {
 int Engine::sync() {
   if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
   harvest();
-  return NK_OK;
+  // a collective the stream ran may have failed on the device (peer.hip: timeout / abort)
+  return (comm && comm->failed()) ? NK_ECOMM : NK_OK;
 }
 
 int Engine::copy(double* dst, const double* src, int64_t cnt) {

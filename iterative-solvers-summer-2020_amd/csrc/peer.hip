@@ -1,0 +1,344 @@
+// Peer-memory communicator for the row-slab decomposition (one process per GPU, xGMI).
+//
+// The slab path's collectives are tiny and latency-bound: per Arnoldi step one 2-row halo of
+// 2 x nx doubles per neighbour and one all-reduce of 2 nv + 3 doubles (SURVEY.md section 5:
+// "latency dominates, not the 153 GB/s link rate").  Through RCCL each costs a library call, its
+// proxy/kernels and their own synchronisation (measured at world size 1: grouped send/recv
+// 25 us).  Here every rank exports ONE fine-grained device buffer (IPC handle
+// exchanged once through any side channel, e.g. torch.distributed); afterwards a collective is
+// one small kernel on the solver's stream that writes straight into the peers' buffers over
+// xGMI and waits for their tagged flags in its own:
+//
+//   halo       each block writes its columns of rows 0, 1 into the previous rank's "hi" staging
+//              rows and rows ny-2, ny-1 into the next rank's "lo" staging rows; the last block to
+//              arrive publishes both flags (release, system scope); every block then waits for
+//              the two flags of its own buffer and copies its staging rows into lo / hi.  With
+//              two ranks (prev == next) the two directions land in different staging rows, so
+//              no posting order matters (the RCCL path needed one, comm.cpp).
+//   allreduce  one block writes the rank's values into slot [rank] of every rank's buffer, then
+//              a flag per rank; it waits for all flags of its own buffer and combines the slots
+//              in rank order (sum, or NaN-propagating max), so every rank computes bitwise the
+//              same result.
+//
+// Tags: each collective kind has its own counter, advanced identically on every rank (all ranks
+// issue the same collectives in the same order).  Slots and flags are double-buffered by tag
+// parity: a rank can only be one collective ahead of any peer (each collective waits for every
+// peer's contribution to the previous one), so parity t & 1 is never overwritten before it was
+// read.  A wait is bounded: after ~20 s, or once any rank aborted the group (its abort word is
+// written into every peer's buffer), the kernel sets the rank's error word (pinned host memory)
+// and returns; the host turns that into NK_ECOMM (Engine::sync), so peers blocked in a
+// collective with a failed rank return instead of hanging (nkhip.h nk_comm_abort).
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/nkhip.h"
+#include "comm.h"
+#include "nk_device.h"
+
+namespace nk {
+namespace {
+
+constexpr int kMaxPeers = 64;
+constexpr int kRedMax = 256;  // values per all-reduce (the fused multi-dot: 2 nv + 3 <= 73)
+constexpr int kHaloBlock = 256;
+
+// byte offsets inside a rank's exported buffer
+constexpr int64_t kOffAbort = 0;                                  // uint64
+constexpr int64_t kOffRedFlag = 64;                               // [2][kMaxPeers] uint64
+constexpr int64_t kOffHaloFlag = kOffRedFlag + 2 * kMaxPeers * 8;  // [2][2] uint64
+constexpr int64_t kOffRedSlot = 2048;                             // [2][P][kRedMax] double
+__host__ __device__ inline int64_t off_stage(int P) {             // [2][2][2][max_nx] double
+  return (kOffRedSlot + int64_t(2) * P * kRedMax * 8 + 255) / 256 * 256;
+}
+__host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
+  return off_stage(P) + int64_t(2) * 2 * 2 * max_nx * 8;
+}
+
+struct PeerArgs {
+  char* base[kMaxPeers];  // every rank's buffer in this address space (mine: base[rank])
+  int P, rank;
+  int64_t max_nx;
+  uint64_t tag;
+  uint32_t* counter;  // arrival counter of the halo kernel's blocks (local, reset by the last)
+  int* err;           // pinned host error word
+};
+
+__device__ __forceinline__ uint64_t* red_flag(char* b, int par, int q) {
+  return reinterpret_cast<uint64_t*>(b + kOffRedFlag) + par * kMaxPeers + q;
+}
+__device__ __forceinline__ uint64_t* halo_flag(char* b, int par, int side) {
+  return reinterpret_cast<uint64_t*>(b + kOffHaloFlag) + par * 2 + side;
+}
+__device__ __forceinline__ double* red_slot(char* b, int P, int par, int q) {
+  return reinterpret_cast<double*>(b + kOffRedSlot) + (int64_t(par) * P + q) * kRedMax;
+}
+// staging rows: side 0 = "lo" (the previous rank's last two rows), 1 = "hi" (the next rank's
+// first two rows)
+__device__ __forceinline__ double* stage(char* b, int P, int64_t max_nx, int par, int side,
+                                         int row) {
+  return reinterpret_cast<double*>(b + off_stage(P)) + ((int64_t(par) * 2 + side) * 2 + row) * max_nx;
+}
+
+constexpr uint64_t kSpinMax = uint64_t(1) << 27;  // polls of ~150 ns: ~20 s
+
+// Wait (one lane) until *flag == tag; false on abort or timeout (error word set).
+__device__ bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
+  const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(a.base[a.rank] + kOffAbort);
+  for (uint64_t n = 0;; ++n) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.tag) return true;
+    if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+        n > kSpinMax) {
+      __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+__global__ void __launch_bounds__(kRedMax) peer_allreduce_kernel(const PeerArgs a, double* dev,
+                                                                 int nsum, int nv) {
+  const int t = threadIdx.x;
+  const int par = int(a.tag & 1);
+  const double v = (t < nv) ? dev[t] : 0.0;
+  if (t < nv)
+    for (int q = 0; q < a.P; ++q) red_slot(a.base[q], a.P, par, a.rank)[t] = v;
+  __threadfence_system();
+  __syncthreads();
+  if (t < a.P)
+    __hip_atomic_store(red_flag(a.base[t], par, a.rank), a.tag, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __shared__ int ok;
+  if (t == 0) ok = 1;
+  __syncthreads();
+  if (t < a.P && !wait_tag(a, red_flag(a.base[a.rank], par, t))) ok = 0;
+  __syncthreads();
+  if (!ok) return;
+  __threadfence_system();
+  if (t < nv) {
+    char* mine = a.base[a.rank];
+    double acc = red_slot(mine, a.P, par, 0)[t];
+    for (int q = 1; q < a.P; ++q) {
+      const double x = red_slot(mine, a.P, par, q)[t];
+      acc = (t < nsum) ? acc + x : nmax(acc, x);
+    }
+    dev[t] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(kHaloBlock) peer_halo_kernel(const PeerArgs a, const double* v,
+                                                               double* lo, double* hi, int64_t ny,
+                                                               int64_t nx) {
+  const int par = int(a.tag & 1);
+  const int prev = (a.rank - 1 + a.P) % a.P, next = (a.rank + 1) % a.P;
+  const int64_t c = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x;
+  if (c < nx) {
+    // my first rows are the previous rank's "hi", my last rows the next rank's "lo"
+    stage(a.base[prev], a.P, a.max_nx, par, 1, 0)[c] = v[c];
+    stage(a.base[prev], a.P, a.max_nx, par, 1, 1)[c] = v[nx + c];
+    stage(a.base[next], a.P, a.max_nx, par, 0, 0)[c] = v[(ny - 2) * nx + c];
+    stage(a.base[next], a.P, a.max_nx, par, 0, 1)[c] = v[(ny - 1) * nx + c];
+  }
+  __threadfence_system();
+  __syncthreads();
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const uint32_t arrived =
+        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {  // every block's rows are out: publish
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(halo_flag(a.base[prev], par, 1), a.tag, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(halo_flag(a.base[next], par, 0), a.tag, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    char* mine = a.base[a.rank];
+    if (!wait_tag(a, halo_flag(mine, par, 0)) || !wait_tag(a, halo_flag(mine, par, 1))) ok = 0;
+  }
+  __syncthreads();
+  if (!ok) return;
+  __threadfence_system();
+  if (c < nx) {
+    char* mine = a.base[a.rank];
+    lo[c] = stage(mine, a.P, a.max_nx, par, 0, 0)[c];
+    lo[nx + c] = stage(mine, a.P, a.max_nx, par, 0, 1)[c];
+    hi[c] = stage(mine, a.P, a.max_nx, par, 1, 0)[c];
+    hi[nx + c] = stage(mine, a.P, a.max_nx, par, 1, 1)[c];
+  }
+}
+
+// what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)
+struct PeerBlob {
+  hipIpcMemHandle_t ipc;
+  uint64_t ptr;  // the buffer in the owner's address space (used when the peer is the same process)
+  int32_t pid, bus, dev, domain;
+  int64_t bytes;
+};
+
+struct PeerComm final : nk_comm {
+  int r = 0, p = 1;
+  int64_t max_nx = 0;
+  char* local = nullptr;  // this rank's exported, fine-grained buffer
+  int64_t bytes = 0;
+  std::vector<char*> base;
+  std::vector<bool> opened;  // base[q] came from hipIpcOpenMemHandle
+  uint32_t* counter = nullptr;
+  int* err = nullptr;  // pinned host
+  hipStream_t side = nullptr;  // abort writes (never queued behind a spinning collective)
+  uint64_t red_tag = 0, halo_tag = 0;
+  bool connected = false, same_dev = false, aborted = false;
+  PeerBlob blob{};
+
+  ~PeerComm() override {
+    for (int q = 0; q < int(base.size()); ++q)
+      if (opened[q]) (void)hipIpcCloseMemHandle(base[q]);
+    if (local) (void)hipFree(local);
+    if (counter) (void)hipFree(counter);
+    if (err) (void)hipHostFree(err);
+    if (side) (void)hipStreamDestroy(side);
+  }
+  int rank() const override { return r; }
+  int size() const override { return p; }
+  bool shares_device() const override { return same_dev; }
+  bool failed() const override {
+    return aborted || (err && __atomic_load_n(err, __ATOMIC_ACQUIRE) != 0);
+  }
+
+  PeerArgs args(uint64_t tag) const {
+    PeerArgs a;
+    for (int q = 0; q < kMaxPeers; ++q) a.base[q] = q < p ? base[q] : nullptr;
+    a.P = p;
+    a.rank = r;
+    a.max_nx = max_nx;
+    a.tag = tag;
+    a.counter = counter;
+    a.err = err;
+    return a;
+  }
+
+  int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
+    if (!connected || failed()) return NK_ECOMM;
+    if (nv <= 0) return NK_OK;
+    if (nv > kRedMax) return NK_EINVAL;
+    hipLaunchKernelGGL(peer_allreduce_kernel, dim3(1), dim3(kRedMax), 0, s, args(++red_tag), dev,
+                       nsum, nv);
+    return hipGetLastError() == hipSuccess ? NK_OK : NK_EHIP;
+  }
+
+  int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
+           hipStream_t s) override {
+    if (!connected || failed()) return NK_ECOMM;
+    if (nx > max_nx || ny < 2) return NK_EINVAL;
+    hipLaunchKernelGGL(peer_halo_kernel, dim3(unsigned((nx + kHaloBlock - 1) / kHaloBlock)),
+                       dim3(kHaloBlock), 0, s, args(++halo_tag), v, lo, hi, ny, nx);
+    return hipGetLastError() == hipSuccess ? NK_OK : NK_EHIP;
+  }
+
+  int barrier(hipStream_t s) override {
+    if (!connected || failed()) return NK_ECOMM;
+    double* d = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double), s) != hipSuccess)
+      return NK_EHIP;
+    int rc = hipMemsetAsync(d, 0, sizeof(double), s) == hipSuccess ? allreduce(d, 1, 1, s) : NK_EHIP;
+    (void)hipFreeAsync(d, s);
+    if (rc) return rc;
+    if (hipStreamSynchronize(s) != hipSuccess) return NK_EHIP;
+    return failed() ? NK_ECOMM : NK_OK;
+  }
+
+  // The group failed: every rank's kernels waiting in a collective leave with the error word
+  // set -- this rank's at once, the peers' through the abort word written into their buffers.
+  void abort() override {
+    if (aborted) return;
+    aborted = true;
+    if (!side) return;
+    static const uint64_t one = 1;
+    for (int q = 0; q < int(base.size()); ++q)
+      if (base[q])
+        (void)hipMemcpyAsync(base[q] + kOffAbort, &one, sizeof(one), hipMemcpyHostToDevice, side);
+    (void)hipStreamSynchronize(side);
+    (void)hipGetLastError();
+  }
+};
+
+}  // namespace
+
+int comm_peer_handle_bytes() { return int(sizeof(PeerBlob)); }
+
+int comm_create_peer(nk_comm** out, int rank, int nranks, int64_t max_nx, void* handle_out) {
+  if (!out || !handle_out || nranks < 1 || nranks > kMaxPeers || rank < 0 || rank >= nranks ||
+      max_nx < 1)
+    return NK_EINVAL;
+  auto c = std::make_unique<PeerComm>();
+  c->r = rank;
+  c->p = nranks;
+  c->max_nx = max_nx;
+  c->bytes = buffer_bytes(nranks, max_nx);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return NK_EHIP;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->local), size_t(c->bytes),
+                            hipDeviceMallocFinegrained) != hipSuccess) {
+    c->local = nullptr;
+    (void)hipGetLastError();
+    return NK_ENOMEM;
+  }
+  if (hipMemset(c->local, 0, size_t(c->bytes)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&c->counter), sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(c->counter, 0, sizeof(uint32_t)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->err), sizeof(int), hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
+    return NK_EHIP;
+  *c->err = 0;
+  PeerBlob& b = c->blob;
+  std::memset(&b, 0, sizeof(b));
+  if (hipIpcGetMemHandle(&b.ipc, c->local) != hipSuccess) {
+    (void)hipGetLastError();  // single-process groups do not need it
+    std::memset(&b.ipc, 0, sizeof(b.ipc));
+  }
+  b.ptr = reinterpret_cast<uint64_t>(c->local);
+  b.pid = int32_t(getpid());
+  (void)hipDeviceGetAttribute(&b.bus, hipDeviceAttributePciBusId, dev);
+  (void)hipDeviceGetAttribute(&b.dev, hipDeviceAttributePciDeviceId, dev);
+  (void)hipDeviceGetAttribute(&b.domain, hipDeviceAttributePciDomainID, dev);
+  b.bytes = c->bytes;
+  std::memcpy(handle_out, &b, sizeof(b));
+  *out = c.release();
+  return NK_OK;
+}
+
+int comm_peer_connect(nk_comm* comm, const void* handles) {
+  auto* c = dynamic_cast<PeerComm*>(comm);
+  if (!c || !handles || c->connected) return NK_EINVAL;
+  const auto* blobs = static_cast<const PeerBlob*>(handles);
+  if (std::memcmp(&blobs[c->r], &c->blob, sizeof(PeerBlob)) != 0) return NK_EINVAL;
+  c->base.assign(c->p, nullptr);
+  c->opened.assign(c->p, false);
+  for (int q = 0; q < c->p; ++q) {
+    const PeerBlob& b = blobs[q];
+    if (b.bytes != c->bytes) return NK_EINVAL;  // every rank built for the same group shape
+    if (q != c->r && b.bus == c->blob.bus && b.dev == c->blob.dev && b.domain == c->blob.domain)
+      c->same_dev = true;
+    if (b.pid == c->blob.pid) {  // this process (the rank itself, or a rank on another thread)
+      c->base[q] = reinterpret_cast<char*>(b.ptr);
+      continue;
+    }
+    void* ptr = nullptr;
+    if (hipIpcOpenMemHandle(&ptr, b.ipc, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      std::fprintf(stderr, "nkhip: peer comm rank %d cannot map rank %d's buffer: %s\n", c->r, q,
+                   hipGetErrorString(hipGetLastError()));
+      return NK_ECOMM;
+    }
+    c->base[q] = static_cast<char*>(ptr);
+    c->opened[q] = true;
+  }
+  c->connected = true;
+  return NK_OK;
+}
+
+}  // namespace nk

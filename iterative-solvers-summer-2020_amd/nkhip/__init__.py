@@ -7,7 +7,7 @@ kernels through the C-ABI library ``libnkhip.so`` (include/nkhip.h).  There is n
 importing this package without the built library raises ImportError.
 """
 from ._lib import NKError, lib, status_string  # noqa: F401
-from .dist import RcclComm, loopback_comms, neighbours, slab_rows  # noqa: F401
+from .dist import PeerComm, RcclComm, loopback_comms, neighbours, peer_comms, slab_rows  # noqa: F401
 from .droplet import Droplet, read_init, write_init  # noqa: F401
 from .mems import Mems  # noqa: F401
 from .ops import (axpy, dot, lap5_apply, maxnorm, maxpy, mdot, nrm2, scal, sh13_apply, stream_copy,  # noqa: F401

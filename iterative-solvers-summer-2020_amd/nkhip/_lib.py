@@ -103,6 +103,9 @@ SIGNATURES = [
     ("nk_comm_get_unique_id", C.c_int, [_P]),
     ("nk_comm_create_rccl", C.c_int, [C.POINTER(_P), _P, _I32, _I32]),
     ("nk_comm_create_loopback", C.c_int, [C.POINTER(_P), _I32]),
+    ("nk_comm_peer_handle_bytes", C.c_int, []),
+    ("nk_comm_create_peer", C.c_int, [C.POINTER(_P), _I32, _I32, _I64, _P]),
+    ("nk_comm_peer_connect", C.c_int, [_P, _P]),
     ("nk_comm_destroy", C.c_int, [_P]),
     ("nk_comm_abort", C.c_int, [_P]),
     ("nk_sh_create", C.c_int, [C.POINTER(_P), _I64, _I64, _I64, _D, _D, _D, _D,

@@ -10,7 +10,8 @@ N x N torus is cut into row slabs, one per rank (one process per GPU):
   fused reduction, so every rank runs the identical host-side Hessenberg algebra.
 
 ``slab_rows`` is plain arithmetic (tested on CPU); ``RcclComm.from_torch_distributed`` shares
-the RCCL unique id through an initialised ``torch.distributed`` process group (gloo or nccl).
+the RCCL unique id through an initialised ``torch.distributed`` process group (gloo or nccl);
+``PeerComm.from_torch_distributed`` exchanges the peer-memory buffers' IPC handles the same way.
 """
 from __future__ import annotations
 
@@ -77,6 +78,54 @@ class RcclComm(Comm):
         obj = [cls.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         return cls.create(obj[0], rank, size)
+
+
+class PeerComm(Comm):
+    """Peer-memory communicator (csrc/peer.hip): every rank exports one fine-grained device
+    buffer; halos and all-reduces are single small kernels that write into the peers' buffers
+    over xGMI and wait for tagged flags -- no RCCL call on the solver's stream.  Works for one
+    process per GPU, several processes on one GPU (IPC on the same device) and several ranks
+    (threads) in one process.  ``max_nx``: the widest slab row any collective will carry."""
+
+    def __init__(self, handle, rank, size, blob=b""):
+        super().__init__(handle, rank, size)
+        self.blob = blob
+
+    @classmethod
+    def create(cls, rank: int, nranks: int, max_nx: int) -> "PeerComm":
+        h = C.c_void_p()
+        buf = (C.c_char * lib.nk_comm_peer_handle_bytes())()
+        check(lib.nk_comm_create_peer(C.byref(h), int(rank), int(nranks), int(max_nx), buf),
+              "nk_comm_create_peer")
+        return cls(h, rank, nranks, bytes(buf))
+
+    def connect(self, blobs):
+        """Map every rank's buffer (``blobs``: each rank's ``blob``, in rank order)."""
+        allb = b"".join(blobs)
+        buf = (C.c_char * len(allb)).from_buffer_copy(allb)
+        check(lib.nk_comm_peer_connect(self.handle, buf), "nk_comm_peer_connect")
+        return self
+
+    @classmethod
+    def from_torch_distributed(cls, max_nx: int, group=None) -> "PeerComm":
+        """Create this rank's side and exchange the handle blobs through an initialised
+        torch.distributed group (any backend)."""
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        c = cls.create(rank, size, max_nx)
+        blobs = [None] * size
+        dist.all_gather_object(blobs, c.blob, group=group)
+        return c.connect(blobs)
+
+
+def peer_comms(nranks: int, max_nx: int):
+    """A peer-memory group of ``nranks`` ranks inside this process (one host thread per slab;
+    the ranks' buffers are mapped directly, no IPC)."""
+    cs = [PeerComm.create(r, nranks, max_nx) for r in range(nranks)]
+    blobs = [c.blob for c in cs]
+    for c in cs:
+        c.connect(blobs)
+    return cs
 
 
 def loopback_comms(nranks: int):

@@ -1,0 +1,27 @@
+#!/bin/bash
+# World-size-1 cost of the slab path: plain periodic slab vs the peer-memory communicator vs
+# RCCL (bench.py --peer-self / --rccl-self), alternating inside one gpurun call.
+#   bash scripts/ab_comm.sh [rounds]
+set -u
+R=${1:-2}
+ARGS="--steps 10 --warmup 2 --extra off --cpu-baseline off"
+mkdir -p gpurun_out
+for i in $(seq 1 "$R"); do
+  for V in plain peer rccl; do
+    case $V in
+      plain) X="" ;;
+      peer) X="--peer-self" ;;
+      rccl) X="--rccl-self" ;;
+    esac
+    timeout -k 10 300 python3 bench.py $ARGS $X > gpurun_out/abc_${V}_$i.log 2>&1 || { echo "$V failed"; tail -5 gpurun_out/abc_${V}_$i.log; exit 1; }
+    python3 - "$V" gpurun_out/abc_${V}_$i.log <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+k = d["kernels"]
+parts = " ".join(f"{n}:{v['avg_us']:.1f}us" for n, v in k.items()
+                 if n in ("halo", "reduce_final", "arnoldi_ctl", "arnoldi_edge", "arnoldi_fused"))
+print(f"{sys.argv[1]:6s} steps/s {d['value']:.3f} ms/arn {d['ms_per_arnoldi_step']:.4f} "
+      f"fused {d['roofline']['frac']:.4f} {parts}")
+PY
+  done
+done
