@@ -176,6 +176,14 @@ int nk_maxpy(const double* const* V_dev, const double* coef, int32_t m, double* 
  * achievable HBM streaming rate (roofline.peak_measured), the ~6.3 TB/s of a float4 copy. */
 int nk_stream_copy(const double* src_dev, double* dst_dev, int64_t n, void* stream);
 
+/* Debugging aid, bounds-checked build only (`make -C iterative-solvers-summer-2020_amd check` ->
+ * nkhip/libnkhip_check.so): every index the fused Arnoldi / slab-edge kernels compute is checked
+ * against its array; an out-of-range index is counted (and replaced by 0, so nothing faults).
+ * *violations = the count since the last reset, *first_line = the smallest arnoldi.hip source
+ * line among them (0: none); reset != 0 clears the counters.  Synchronises the device.
+ * NK_EINVAL from the product library (no checks compiled in). */
+int nk_debug_bounds(int64_t* violations, int32_t* first_line, int32_t reset);
+
 /* ---------------- communicators (row-slab decomposition over RCCL / xGMI) ---------------- */
 int nk_comm_unique_id_bytes(void);
 int nk_comm_get_unique_id(void* out);

@@ -13,6 +13,7 @@
 
 #include "nk_device.h"
 #include "nk_kernels.h"
+#include "peer_dev.h"
 
 namespace nk {
 namespace {
@@ -202,6 +203,35 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
   ctl_body(S, H, result, nullptr, prm, status, t);
 }
 
+// Row slabs over the peer-memory communicator: the reduction, the all-reduce of its nval sums
+// (peer_dev.h, one wave writing into every rank's buffer over xGMI) and the control of step t in
+// ONE launch -- the three launches (reduce, peer all-reduce, control) of the generic path.  Every
+// rank's last block computes the same all-reduced values, so every rank's control takes the same
+// decisions.  A failed all-reduce (a peer aborted or timed out) halts the queued fused step and
+// leaves status[t] unset; the host's wait then finds the communicator failed.
+__global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
+    const double* partial, int64_t nblk, double* result, double* result_host, const PeerArgs pa,
+    ArnCtlState* S, ArnCtlState* H, double* prm, uint32_t* status, int t) {
+  const int k = blockIdx.x;
+  const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, true);
+  __shared__ bool last;
+  if (threadIdx.x == 0) {
+    result[k] = s;
+    __threadfence();
+    last = atomicAdd(&S->arrive, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= 64) return;
+  __threadfence();
+  if (threadIdx.x == 0) S->arrive = 0;
+  if (!peer_allreduce_wave(pa, result, int(gridDim.x), int(gridDim.x))) {
+    if (threadIdx.x == 0) prm[kArnMaxNV + 3] = 1.0;  // the queued fused step does nothing
+    return;
+  }
+  __threadfence();  // the combined values (other lanes' stores) before the control reads them
+  ctl_body(S, H, result, result_host, prm, status, t);
+}
+
 }  // namespace
 
 hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
@@ -219,6 +249,18 @@ hipError_t arn_reduce_ctl_launch(const double* partial, int64_t nblk, int nval, 
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(arn_reduce_ctl_kernel, dim3(unsigned(nval)), dim3(RB), 0, s, partial, nblk,
                      result, result_host, S, H, prm, status, t);
+  return hipGetLastError();
+}
+
+hipError_t arn_reduce_allreduce_ctl_launch(const double* partial, int64_t nblk, int nval,
+                                           double* result, double* result_host, const PeerArgs& pa,
+                                           ArnCtlState* S, ArnCtlState* H, double* prm,
+                                           uint32_t* status, int t, hipStream_t s) {
+  if (!partial || !result || !S || !H || !prm || !status || nval < 1 || nval > kRedMax || t < 0 ||
+      t > kMaxVec || pa.P < 1 || pa.P > kMaxPeers)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(arn_reduce_allreduce_ctl_kernel, dim3(unsigned(nval)), dim3(RB), 0, s,
+                     partial, nblk, result, result_host, pa, S, H, prm, status, t);
   return hipGetLastError();
 }
 

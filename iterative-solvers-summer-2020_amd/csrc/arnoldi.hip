@@ -35,6 +35,7 @@
 
 #include "nk_device.h"
 #include "nk_kernels.h"
+#include "peer_dev.h"
 
 namespace nk {
 namespace {
@@ -71,6 +72,39 @@ __device__ __forceinline__ double gld(const double* p) { return *(gdouble*)p; }
 // Stores through a raw buffer resource: a lane whose offset is out of range (kOOB) writes
 // nothing, so masked stores need no branch.
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
+
+// Bounds-checked build (`make check` -> nkhip/libnkhip_check.so, -DNKHIP_ARN_CHECK; GPU
+// AddressSanitizer is not available on this pool).  Every index the fused kernels compute --
+// row and column of each streamed load, block-halo and edge-array offsets, slab halo rows,
+// mailbox records, store offsets, partial-sum slots -- goes through CI()/ARN_CHK(): an index out
+// of its array is counted (per lane, with the first source line) and replaced by 0, so the
+// kernel cannot fault and the host reads the counters afterwards (nk_debug_bounds).  In the
+// product build both are no-ops.
+#ifdef NKHIP_ARN_CHECK
+// [lane]: violations, [64 + lane]: 2^32 - the smallest line (all zero: nothing recorded)
+__device__ unsigned long long g_arn_chk[128];
+__device__ __forceinline__ void arn_chk(bool ok, int line) {
+  if (!ok) {
+    const int l = int(threadIdx.x & 63);  // a per-lane address: vector atomics
+    atomicAdd(&g_arn_chk[l], 1ull);
+    atomicMax(&g_arn_chk[64 + l], (1ull << 32) - (unsigned long long)line);
+  }
+}
+__device__ __forceinline__ int64_t chk_idx(int64_t i, int64_t lim, int line) {
+  const bool ok = i >= 0 && i < lim;
+  arn_chk(ok, line);
+  return ok ? i : 0;
+}
+#define ARN_CHK(c) arn_chk((c), __LINE__)
+#else
+#define ARN_CHK(c) ((void)0)
+__device__ __forceinline__ int64_t chk_idx(int64_t i, int64_t, int) { return i; }
+#endif
+// element index i of an array of lim elements (a 16-B pair load: lim - 1)
+#define CI(i, lim) chk_idx((i), (lim), __LINE__)
+// a buffer-resource store offset (bytes; kOOB = masked) of a 16-B record into lim elements
+#define CO(off, lim) \
+  uint32_t((off) == kOOB ? kOOB : uint32_t(8 * chk_idx(int64_t(off) / 8, (lim) - 1, __LINE__)))
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(double* p, int64_t n) {
@@ -325,7 +359,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const int64_t grpR = (grp + 1 < ngroups) ? grp + 1 : 0;
   // edge-array stores of the outputs: the lane holding columns B, B+1 of a boundary B writes
   // them as E[b][q][2..3]; the lane holding B-2, B-1 as E[b][q][0..1] (b = 0 for nx - 2, nx - 1)
-  const int64_t nbE = ngroups;
+  const int64_t nbE = edge_groups(nx);  // (the 2-wave mailbox blocks are narrower than a group)
+  const int64_t nelem = ny * nx, eelem = edge_elems(ny, nx);
   const bool eL = own && (c % kEdgeW == 0);
   const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
   const int64_t ebo = eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
@@ -334,7 +369,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
   // byte offset of this lane's edge pair at row q (kOOB: nothing to store)
   auto eoff = [&](int64_t q) -> uint32_t {
-    return eOn ? uint32_t(((ebo / 4) * ny * 4 + q * 4 + (ebo & 3)) * 8) : kOOB;
+    return eOn ? uint32_t(CI((ebo / 4) * ny * 4 + q * 4 + (ebo & 3), eelem - 1) * 8) : kOOB;
   };
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
   // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their u arrives in A.yh (the x0 entry
@@ -371,6 +406,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   auto poll = [&](int64_t q, u32x4* a, u32x4* b) {  // issue the two record loads of row q
     const bool on = mb_need(q) && !mb_dead;
     const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+    ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
     *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
     *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
   };
@@ -381,7 +417,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   };
   auto cfd = [&](int e) -> double { return e < NV ? arn_c(A, e) : (e == NV ? a_tau : 0.0); };
   auto recompute = [&](int64_t q) -> dv2 {
-    const int64_t o2 = wrap(q) * nx + fcol;
+    const int64_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
     double p0x = 0.0, p0y = 0.0, p1x = 0.0, p1y = 0.0;
 #pragma unroll 1
     for (int k = 0; k < NI; ++k) {
@@ -427,24 +463,28 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   };
   auto load = [&](Slot& s, int64_t q) {
     const int64_t qq = wrap(q);
-    const int64_t o = qq * nx + col;
+    const int64_t o = CI(qq * nx + col, nelem - 1);
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
     const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
+    const int64_t yo = CI(hq * nx + col, 4 * nx - 1);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const double* a = ep[k] + o;
-      if (k == EX / 2) a = (hrow && hf == (EX & 1)) ? yhb + hq * nx + col : a;
+      if (k == EX / 2) a = (hrow && hf == (EX & 1)) ? yhb + yo : a;
       s.e[k] = gld2<NT>(a);
     }
-    const int64_t ho = qq * nx + hcol;
+    const int64_t ho = CI(qq * nx + hcol, nelem);
     // block halo: from the entry's edge array (four rows per line) or from the vector itself;
     // with the mailbox a load of one fixed line (keeps the row's load batch the same shape)
-    const int64_t eo = ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh;
-    if constexpr (!EXT && !mb) s.hv = gld(useE ? hE + eo : hp + ho);
+    if constexpr (!EXT && !mb) {
+      const int64_t eo = CI(useE ? ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh : 0, eelem);
+      s.hv = gld(useE ? hE + eo : hp + ho);
+    }
     // z on the halo columns (EXT, lanes 4..); u of a slab halo row (A.yh, lanes 0-3); every
     // other lane one fixed line
-    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : (mb ? yhb : hxp + ho));
+    const int64_t hyo = CI(hq * nx + hcol, 4 * nx);
+    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? yhb : hxp + ho));
     s.own = !hrow;
   };
   // entry e of this row for both halves (e is a compile-time index)
@@ -496,6 +536,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       if constexpr (mb) {
         const bool pq = prod && s.own;
         const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
+        ARN_CHK(!pq || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
                                                kMBCoh);
@@ -561,10 +602,10 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const bool st = own && hf == 0 && q >= r0 && q < r1;
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
-                                           st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
+                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
     if (A.Eout_v)  // wave-uniform
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
-                                             st ? eoff(q) : kOOB, 0, 0);
+                                             st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
     return dv2{cm2 + cp2, cm1 + cp3};  // h2 of row q
   };
 
@@ -599,7 +640,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           (in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB,
+                                           CO((in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB, nelem),
                                            0, 0);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
@@ -696,6 +737,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   if (l == 0) {
     const int64_t nw = A.pstride;  // every wave of every block writes a column
     double* p = A.partial + A.pcol0 + gw;
+    ARN_CHK(A.pcol0 + gw < nw && (2 * int64_t(NV) + 2) * nw + A.pcol0 + gw < A.partial_cap);
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int e = 2 * k + hf;
@@ -792,6 +834,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   }
   const bool useE = A.E[0] != nullptr;
   const int64_t nbE = edge_groups(nx);
+  const int64_t nelem = ny * nx, eelem = edge_elems(ny, nx);
   const int64_t bL = B0 / kEdgeW, bR = ((B0 + W * kWW) / kEdgeW) % nbE;
   const bool eL = own && (c % kEdgeW == 0);
   const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
@@ -801,7 +844,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
   const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
   auto eoff = [&](int64_t q) -> uint32_t {
-    return eOn ? uint32_t(((ebo / 4) * ny * 4 + q * 4 + (ebo & 3)) * 8) : kOOB;
+    return eOn ? uint32_t(CI((ebo / 4) * ny * 4 + q * 4 + (ebo & 3), eelem - 1) * 8) : kOOB;
   };
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
   const bool slab = A.yh != nullptr;
@@ -833,11 +876,12 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   auto poll = [&](int64_t q, u32x4* a, u32x4* b) {
     const bool on = mb_need(q) && !mb_dead;
     const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+    ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
     *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
     *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
   };
   auto recompute = [&](int64_t q) -> dv2 {  // push()'s update sum, entry order (rolled loop)
-    const int64_t o2 = wrap(q) * nx + fcol;
+    const int64_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
     dv2 v{0.0, 0.0};
 #pragma unroll 1
     for (int e = 0; e <= NV; ++e) {
@@ -877,20 +921,24 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   };
   auto load = [&](Slot& s, int64_t q) {
     const int64_t qq = wrap(q);
-    const int64_t o = qq * nx + col;
+    const int64_t o = CI(qq * nx + col, nelem - 1);
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
     const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
+    const int64_t yo = CI(hq * nx + col, 4 * nx - 1);
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const double* a = src(e) + o;
-      if (e == EX) a = hrow ? yhb + hq * nx + col : a;
+      if (e == EX) a = hrow ? yhb + yo : a;
       s.e[e] = gld2<NT>(a);
     }
-    const int64_t ho = qq * nx + hcol;
-    const int64_t eo = ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh;
-    if constexpr (!EXT && !mb) s.hv = gld(useE ? hE + eo : hp + ho);
-    s.hx = gld((hrow && lane < 4) ? yhb + hq * nx + hcol : (mb ? yhb : hxp + ho));
+    const int64_t ho = CI(qq * nx + hcol, nelem);
+    if constexpr (!EXT && !mb) {
+      const int64_t eo = CI(useE ? ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh : 0, eelem);
+      s.hv = gld(useE ? hE + eo : hp + ho);
+    }
+    const int64_t hyo = CI(hq * nx + hcol, 4 * nx);
+    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? yhb : hxp + ho));
     s.own = !hrow;
   };
   auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
@@ -923,6 +971,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
       if constexpr (mb) {
         const bool pq = prod && s.own;
         const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
+        ARN_CHK(!pq || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
                                                kMBCoh);
@@ -979,10 +1028,10 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     vw[4] = v;
     const bool st = own && q >= r0 && q < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
-                                           st ? uint32_t((q * nx + col) * 8) : kOOB, 0, 0);
+                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
     if (A.Eout_v)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
-                                             st ? eoff(q) : kOOB, 0, 0);
+                                             st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
     return dv2{cm2 + cp2, cm1 + cp3};
   };
 
@@ -1013,7 +1062,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           in ? uint32_t((r * nx + col) * 8) : kOOB, 0, 0);
+                                           CO(in ? uint32_t((r * nx + col) * 8) : kOOB, nelem), 0, 0);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
                                              in ? eoff(r) : kOOB, 0, 0);
@@ -1086,6 +1135,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   if (lane == 0) {
     const int64_t nw = A.pstride;
     double* p = A.partial + A.pcol0 + gw;
+    ARN_CHK(A.pcol0 + gw < nw && (2 * int64_t(NV) + 2) * nw + A.pcol0 + gw < A.partial_cap);
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       p[int64_t(i) * nw] = aw[i];
@@ -1262,16 +1312,21 @@ hipError_t launch_e(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
 // 4, .. of [V_0 .. V_{nv-1}, w] in one partial, 1, 3, 5, .. in the other, then their sum; for the
 // wide layout (h0 = nv + 1) all entries in order -- so a halo row
 // equals the row its owner computes.
-template <int NV>
+// PEER (row slabs over the peer-memory communicator): the kernel also performs the halo exchange
+// -- it writes its rows straight into the neighbours' staging rows (peer_dev.h), publishes,
+// waits for its own and copies them into yh (lo = rows 0, 1, hi = rows 2, 3) -- one launch
+// instead of this kernel plus the communicator's halo kernel.  A halted step (handed back by the
+// device control, identically on every rank) exchanges nothing on any rank.
+template <int NV, bool PEER>
 __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, double* y4,
-                                                           int h0) {
+                                                           int h0, const PeerArgs pa) {
   const double a_tau = arn_tau(A);
   if (arn_halted(A)) return;
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (j >= A.nx) return;
+  if (!PEER && j >= A.nx) return;
   const int t = blockIdx.y;
   const int64_t row = (t < 2) ? t : A.ny - 4 + t;
-  const int64_t o = row * A.nx + j;
+  const int64_t o = CI(row * A.nx + (j < A.nx ? j : 0), A.ny * A.nx);
   double y;  // the stencil input u of the fused kernel
   if (A.z) {
     y = A.z[o];
@@ -1297,17 +1352,31 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
     }
     y = p0 + p1;
   }
-  y4[int64_t(t) * A.nx + j] = y;
+  if constexpr (!PEER) {
+    y4[int64_t(t) * A.nx + j] = y;
+  } else {
+    // rows 0, 1 are the previous rank's "hi" staging rows, rows ny-2, ny-1 the next rank's "lo"
+    const int par = int(pa.tag & 1);
+    const int q = (t < 2) ? (pa.rank - 1 + pa.P) % pa.P : (pa.rank + 1) % pa.P;
+    ARN_CHK(j >= A.nx || j < pa.max_nx);
+    if (j < A.nx) stage(pa.base[q], pa.P, pa.max_nx, par, t < 2 ? 1 : 0, t & 1)[j] = y;
+    (void)peer_halo_finish(pa, j, A.nx, y4, y4 + 2 * A.nx);  // failure: the host finds it
+  }
 }
 
 template <int NV = 1>
-hipError_t edge_launch_nv(const ArnoldiArgs& A, double* y4, int h0, hipStream_t s) {
+hipError_t edge_launch_nv(const ArnoldiArgs& A, double* y4, int h0, const PeerArgs* pa,
+                          hipStream_t s) {
   if constexpr (NV > kArnMaxNV) {
     return hipErrorInvalidValue;
   } else {
-    if (A.nv != NV) return edge_launch_nv<NV + 1>(A, y4, h0, s);
-    hipLaunchKernelGGL(arnoldi_edge_kernel<NV>, dim3(unsigned((A.nx + 255) / 256), 4), dim3(256),
-                       0, s, A, y4, h0);
+    if (A.nv != NV) return edge_launch_nv<NV + 1>(A, y4, h0, pa, s);
+    const dim3 grid(unsigned((A.nx + 255) / 256), 4);
+    if (pa)
+      hipLaunchKernelGGL((arnoldi_edge_kernel<NV, true>), grid, dim3(256), 0, s, A, y4, h0, *pa);
+    else
+      hipLaunchKernelGGL((arnoldi_edge_kernel<NV, false>), grid, dim3(256), 0, s, A, y4, h0,
+                         PeerArgs{});
     return hipGetLastError();
   }
 }
@@ -1347,7 +1416,14 @@ int edge_split_point(int nv) {
 
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s) {
   if (A.ny < 4 || A.nx < 1 || !y4) return hipErrorInvalidValue;
-  return edge_launch_nv(A, y4, edge_split_point(A.nv), s);
+  return edge_launch_nv(A, y4, edge_split_point(A.nv), nullptr, s);
+}
+
+hipError_t arnoldi_edge_halo_launch(const ArnoldiArgs& A, const PeerArgs& pa, double* yh,
+                                    hipStream_t s) {
+  if (A.ny < 4 || A.nx < 1 || !yh || A.nx > pa.max_nx || pa.P < 1 || pa.P > kMaxPeers)
+    return hipErrorInvalidValue;
+  return edge_launch_nv(A, yh, edge_split_point(A.nv), &pa, s);
 }
 
 int64_t arnoldi_mbox_launches() { return g_mbox_launches.load(std::memory_order_relaxed); }
@@ -1376,6 +1452,35 @@ hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) 
   if (!al) return hipErrorInvalidValue;  // 16-B loads and stores
   if (A.z) return launch_e<true>(A, s, nwaves);
   return launch_e<false>(A, s, nwaves);
+}
+
+int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset) {
+#ifdef NKHIP_ARN_CHECK
+  unsigned long long c[128];
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(c, HIP_SYMBOL(g_arn_chk), sizeof(c), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -2;
+  int64_t n = 0;
+  unsigned long long m = 0;
+  for (int l = 0; l < 64; ++l) {
+    n += int64_t(c[l]);
+    m = (c[64 + l] > m) ? c[64 + l] : m;
+  }
+  if (violations) *violations = n;
+  if (first_line) *first_line = n ? int32_t((1ull << 32) - m) : 0;
+  if (reset) {
+    for (int l = 0; l < 128; ++l) c[l] = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_arn_chk), c, sizeof(c), 0, hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return -2;
+  }
+  return 0;
+#else
+  (void)violations;
+  (void)first_line;
+  (void)reset;
+  return -1;  // not the bounds-checked build
+#endif
 }
 
 }  // namespace nk

@@ -361,6 +361,11 @@ int nk_stream_copy(const double* src, double* dst, int64_t n, void* stream) {
   return hip_rc(stream_copy_launch(src, dst, n, S(stream)));
 }
 
+int nk_debug_bounds(int64_t* violations, int32_t* first_line, int32_t reset) {
+  const int rc = arnoldi_check_counters(violations, first_line, reset != 0);
+  return rc == 0 ? NK_OK : (rc == -1 ? NK_EINVAL : NK_EHIP);
+}
+
 // ------------------------------------------------------------------------------ comms
 int nk_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
 int nk_comm_get_unique_id(void* out) { return out ? comm_get_unique_id(out) : NK_EINVAL; }

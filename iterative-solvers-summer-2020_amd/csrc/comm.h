@@ -11,6 +11,10 @@
 
 #include <cstdint>
 
+namespace nk {
+struct PeerArgs;  // peer_dev.h
+}
+
 struct nk_comm {
   virtual ~nk_comm() = default;
   virtual int rank() const = 0;
@@ -33,6 +37,13 @@ struct nk_comm {
   // a collective already enqueued on the device failed (peer-memory communicator: a wait timed
   // out or the group was aborted); checked after each stream synchronisation (Engine::sync)
   virtual bool failed() const { return false; }
+  // Peer-memory communicator only: the arguments of the NEXT all-reduce of nv values / halo
+  // exchange of nx columns, for a kernel that runs the collective inside its own launch
+  // (arnctl.hip: reduction + all-reduce + Arnoldi control; arnoldi.hip: slab edge rows + halo).
+  // The collective's tag advances exactly as allreduce() / halo() would advance it, so every
+  // rank must take the same sequence.  false: not available (the caller uses allreduce / halo).
+  virtual bool take_allreduce(nk::PeerArgs* /*out*/, int /*nv*/) { return false; }
+  virtual bool take_halo(nk::PeerArgs* /*out*/, int64_t /*nx*/) { return false; }
 };
 
 namespace nk {

@@ -32,6 +32,7 @@
 #include <cstring>
 
 #include "nk_solver.h"
+#include "peer_dev.h"
 
 namespace nk {
 
@@ -434,6 +435,13 @@ int NewtonKrylov::device_steps() {
       return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
         return arn_reduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
                                      E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
+      });
+    PeerArgs pa;  // peer-memory slabs: reduction, all-reduce and control in one launch
+    if (peer_fuse_enabled() && E_.comm->take_allreduce(&pa, nval))
+      return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
+        return arn_reduce_allreduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
+                                               E_.hres_mut(slot), pa, dS_, hS_, prm_, status_,
+                                               t + 1, E_.s);
       });
     rc = E_.reduce_async(nw, nval, nval, slot, false);
     return rc ? rc : control(t + 1, true);

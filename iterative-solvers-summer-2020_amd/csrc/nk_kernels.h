@@ -12,6 +12,12 @@
 
 namespace nk {
 
+struct PeerArgs;  // peer_dev.h (the peer-memory communicator's device-side arguments)
+// Row slabs over the peer-memory communicator run their collectives inside the kernels around
+// them (arnoldi_edge_halo_launch, arn_reduce_allreduce_ctl_launch); NKHIP_PEER_FUSE=0 (read per
+// call) keeps the separate communicator launches.
+bool peer_fuse_enabled();
+
 // ---------------------------------------------------------------------------------------------
 struct Field {
   const double* base;  // rows [0, ny)
@@ -196,6 +202,15 @@ hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves);
 // u = v (or z) on the slab's edge rows 0, 1, ny-2, ny-1 into y4 (4 rows of nx),
 // with the fused kernel's summation order: what the neighbours need as their halo rows
 hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
+// Bounds-checked build only (`make check`, -DNKHIP_ARN_CHECK): indices of the fused / edge kernels
+// that fell outside their arrays since the last reset, and the smallest arnoldi.hip source line
+// among them.  0 = ok, -1 = not the checked build, -2 = HIP error.
+// The same for row slabs over the peer-memory communicator (pa = nk_comm::take_halo), with the
+// halo exchange in the same launch: yh (4 rows of nx) receives the neighbours' rows -- lo = the
+// previous rank's rows ny-2, ny-1, hi = the next rank's rows 0, 1 -- the fused pass's halo rows.
+hipError_t arnoldi_edge_halo_launch(const ArnoldiArgs& A, const PeerArgs& pa, double* yh,
+                                    hipStream_t s);
+int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset);
 
 // ---------------------------------------------------------------------------------------------
 // Device-side Arnoldi control (arnctl.hip, lgmres.cpp).  The loop state of one LGMRES call: the
@@ -245,5 +260,12 @@ hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, dou
 hipError_t arn_reduce_ctl_launch(const double* partial, int64_t nblk, int nval, double* result,
                                  double* result_host, ArnCtlState* S, ArnCtlState* H, double* prm,
                                  uint32_t* status, int t, hipStream_t s);
+// The same for row slabs over the peer-memory communicator (pa = nk_comm::take_allreduce): the
+// reduction, the all-reduce of the nval sums and the control in one launch; result_host (pinned)
+// receives the all-reduced values (the host reads them when the step is handed back).
+hipError_t arn_reduce_allreduce_ctl_launch(const double* partial, int64_t nblk, int nval,
+                                           double* result, double* result_host, const PeerArgs& pa,
+                                           ArnCtlState* S, ArnCtlState* H, double* prm,
+                                           uint32_t* status, int t, hipStream_t s);
 
 }  // namespace nk

@@ -31,6 +31,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -38,66 +39,10 @@
 #include "../../include/nkhip.h"
 #include "comm.h"
 #include "nk_device.h"
+#include "peer_dev.h"
 
 namespace nk {
 namespace {
-
-constexpr int kMaxPeers = 64;
-constexpr int kRedMax = 256;  // values per all-reduce (the fused multi-dot: 2 nv + 3 <= 73)
-constexpr int kHaloBlock = 256;
-
-// byte offsets inside a rank's exported buffer
-constexpr int64_t kOffAbort = 0;                                  // uint64
-constexpr int64_t kOffRedFlag = 64;                               // [2][kMaxPeers] uint64
-constexpr int64_t kOffHaloFlag = kOffRedFlag + 2 * kMaxPeers * 8;  // [2][2] uint64
-constexpr int64_t kOffRedSlot = 2048;                             // [2][P][kRedMax] double
-__host__ __device__ inline int64_t off_stage(int P) {             // [2][2][2][max_nx] double
-  return (kOffRedSlot + int64_t(2) * P * kRedMax * 8 + 255) / 256 * 256;
-}
-__host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
-  return off_stage(P) + int64_t(2) * 2 * 2 * max_nx * 8;
-}
-
-struct PeerArgs {
-  char* base[kMaxPeers];  // every rank's buffer in this address space (mine: base[rank])
-  int P, rank;
-  int64_t max_nx;
-  uint64_t tag;
-  uint32_t* counter;  // arrival counter of the halo kernel's blocks (local, reset by the last)
-  int* err;           // pinned host error word
-};
-
-__device__ __forceinline__ uint64_t* red_flag(char* b, int par, int q) {
-  return reinterpret_cast<uint64_t*>(b + kOffRedFlag) + par * kMaxPeers + q;
-}
-__device__ __forceinline__ uint64_t* halo_flag(char* b, int par, int side) {
-  return reinterpret_cast<uint64_t*>(b + kOffHaloFlag) + par * 2 + side;
-}
-__device__ __forceinline__ double* red_slot(char* b, int P, int par, int q) {
-  return reinterpret_cast<double*>(b + kOffRedSlot) + (int64_t(par) * P + q) * kRedMax;
-}
-// staging rows: side 0 = "lo" (the previous rank's last two rows), 1 = "hi" (the next rank's
-// first two rows)
-__device__ __forceinline__ double* stage(char* b, int P, int64_t max_nx, int par, int side,
-                                         int row) {
-  return reinterpret_cast<double*>(b + off_stage(P)) + ((int64_t(par) * 2 + side) * 2 + row) * max_nx;
-}
-
-constexpr uint64_t kSpinMax = uint64_t(1) << 27;  // polls of ~150 ns: ~20 s
-
-// Wait (one lane) until *flag == tag; false on abort or timeout (error word set).
-__device__ bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
-  const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(a.base[a.rank] + kOffAbort);
-  for (uint64_t n = 0;; ++n) {
-    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.tag) return true;
-    if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-        n > kSpinMax) {
-      __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-}
 
 __global__ void __launch_bounds__(kRedMax) peer_allreduce_kernel(const PeerArgs a, double* dev,
                                                                  int nsum, int nv) {
@@ -142,34 +87,7 @@ __global__ void __launch_bounds__(kHaloBlock) peer_halo_kernel(const PeerArgs a,
     stage(a.base[next], a.P, a.max_nx, par, 0, 0)[c] = v[(ny - 2) * nx + c];
     stage(a.base[next], a.P, a.max_nx, par, 0, 1)[c] = v[(ny - 1) * nx + c];
   }
-  __threadfence_system();
-  __syncthreads();
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    ok = 1;
-    const uint32_t arrived =
-        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {  // every block's rows are out: publish
-      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      __hip_atomic_store(halo_flag(a.base[prev], par, 1), a.tag, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(halo_flag(a.base[next], par, 0), a.tag, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    char* mine = a.base[a.rank];
-    if (!wait_tag(a, halo_flag(mine, par, 0)) || !wait_tag(a, halo_flag(mine, par, 1))) ok = 0;
-  }
-  __syncthreads();
-  if (!ok) return;
-  __threadfence_system();
-  if (c < nx) {
-    char* mine = a.base[a.rank];
-    lo[c] = stage(mine, a.P, a.max_nx, par, 0, 0)[c];
-    lo[nx + c] = stage(mine, a.P, a.max_nx, par, 0, 1)[c];
-    hi[c] = stage(mine, a.P, a.max_nx, par, 1, 0)[c];
-    hi[nx + c] = stage(mine, a.P, a.max_nx, par, 1, 1)[c];
-  }
+  peer_halo_finish(a, c, nx, lo, hi);
 }
 
 // what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)
@@ -230,6 +148,17 @@ struct PeerComm final : nk_comm {
     return hipGetLastError() == hipSuccess ? NK_OK : NK_EHIP;
   }
 
+  bool take_allreduce(PeerArgs* out, int nv) override {
+    if (!connected || failed() || nv < 1 || nv > kRedMax) return false;
+    *out = args(++red_tag);
+    return true;
+  }
+  bool take_halo(PeerArgs* out, int64_t nx) override {
+    if (!connected || failed() || nx > max_nx) return false;
+    *out = args(++halo_tag);
+    return true;
+  }
+
   int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,
            hipStream_t s) override {
     if (!connected || failed()) return NK_ECOMM;
@@ -267,6 +196,11 @@ struct PeerComm final : nk_comm {
 };
 
 }  // namespace
+
+bool peer_fuse_enabled() {
+  const char* e = std::getenv("NKHIP_PEER_FUSE");
+  return !(e && e[0] == '0');
+}
 
 int comm_peer_handle_bytes() { return int(sizeof(PeerBlob)); }
 

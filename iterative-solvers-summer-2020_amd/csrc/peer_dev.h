@@ -1,0 +1,143 @@
+// Device-side layout and primitives of the peer-memory communicator (peer.hip), shared with the
+// kernels that run a collective inside their own launch (arnctl.hip: reduction + all-reduce +
+// Arnoldi control; arnoldi.hip: slab edge rows + halo exchange).  See peer.hip for the protocol.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "nk_device.h"
+
+namespace nk {
+
+constexpr int kMaxPeers = 64;
+constexpr int kRedMax = 256;  // values per all-reduce (the fused multi-dot: 2 nv + 3 <= 73)
+constexpr int kHaloBlock = 256;
+
+// byte offsets inside a rank's exported buffer
+constexpr int64_t kOffAbort = 0;                                  // uint64
+constexpr int64_t kOffRedFlag = 64;                               // [2][kMaxPeers] uint64
+constexpr int64_t kOffHaloFlag = kOffRedFlag + 2 * kMaxPeers * 8;  // [2][2] uint64
+constexpr int64_t kOffRedSlot = 2048;                             // [2][P][kRedMax] double
+__host__ __device__ inline int64_t off_stage(int P) {             // [2][2][2][max_nx] double
+  return (kOffRedSlot + int64_t(2) * P * kRedMax * 8 + 255) / 256 * 256;
+}
+__host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
+  return off_stage(P) + int64_t(2) * 2 * 2 * max_nx * 8;
+}
+
+struct PeerArgs {
+  char* base[kMaxPeers];  // every rank's buffer in this address space (mine: base[rank])
+  int P, rank;
+  int64_t max_nx;
+  uint64_t tag;
+  uint32_t* counter;  // arrival counter of the halo kernel's blocks (local, reset by the last)
+  int* err;           // pinned host error word
+};
+
+__device__ __forceinline__ uint64_t* red_flag(char* b, int par, int q) {
+  return reinterpret_cast<uint64_t*>(b + kOffRedFlag) + par * kMaxPeers + q;
+}
+__device__ __forceinline__ uint64_t* halo_flag(char* b, int par, int side) {
+  return reinterpret_cast<uint64_t*>(b + kOffHaloFlag) + par * 2 + side;
+}
+__device__ __forceinline__ double* red_slot(char* b, int P, int par, int q) {
+  return reinterpret_cast<double*>(b + kOffRedSlot) + (int64_t(par) * P + q) * kRedMax;
+}
+// staging rows: side 0 = "lo" (the previous rank's last two rows), 1 = "hi" (the next rank's
+// first two rows)
+__device__ __forceinline__ double* stage(char* b, int P, int64_t max_nx, int par, int side,
+                                         int row) {
+  return reinterpret_cast<double*>(b + off_stage(P)) + ((int64_t(par) * 2 + side) * 2 + row) * max_nx;
+}
+
+constexpr uint64_t kSpinMax = uint64_t(1) << 27;  // polls of ~150 ns: ~20 s
+
+// Wait (one lane) until *flag == tag; false on abort or timeout (error word set).
+__device__ inline bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
+  const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(a.base[a.rank] + kOffAbort);
+  for (uint64_t n = 0;; ++n) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.tag) return true;
+    if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+        n > kSpinMax) {
+      __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// The second half of a halo exchange, called by every block of the grid after the block wrote
+// its part of the neighbours' staging rows (thread c of a block with blockIdx.y == 0: column c):
+// the last block to arrive publishes both neighbours' flags (release, system scope), every block
+// waits for its own two flags, and the blockIdx.y == 0 blocks copy their columns of the staged
+// rows into lo / hi (2 rows of nx each).  false: a peer failed or timed out (error word set, lo / hi untouched).
+__device__ inline bool peer_halo_finish(const PeerArgs& a, int64_t c, int64_t nx, double* lo,
+                                        double* hi) {
+  const int par = int(a.tag & 1);
+  const int prev = (a.rank - 1 + a.P) % a.P, next = (a.rank + 1) % a.P;
+  __threadfence_system();
+  __syncthreads();
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const uint32_t arrived =
+        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x * gridDim.y - 1) {  // every block's rows are out: publish
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(halo_flag(a.base[prev], par, 1), a.tag, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(halo_flag(a.base[next], par, 0), a.tag, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    char* mine = a.base[a.rank];
+    if (!wait_tag(a, halo_flag(mine, par, 0)) || !wait_tag(a, halo_flag(mine, par, 1))) ok = 0;
+  }
+  __syncthreads();
+  if (!ok) return false;
+  __threadfence_system();
+  if (c < nx && blockIdx.y == 0) {
+    char* mine = a.base[a.rank];
+    lo[c] = stage(mine, a.P, a.max_nx, par, 0, 0)[c];
+    lo[nx + c] = stage(mine, a.P, a.max_nx, par, 0, 1)[c];
+    hi[c] = stage(mine, a.P, a.max_nx, par, 1, 0)[c];
+    hi[nx + c] = stage(mine, a.P, a.max_nx, par, 1, 1)[c];
+  }
+  return true;
+}
+
+// One wave (lanes 0..63 of the calling block; the caller's other waves take no part): v[0, nv)
+// summed (k < nsum) or NaN-propagating max-reduced over the ranks, in rank order (bitwise the
+// same on every rank), in place.  false: a peer failed or timed out (error word set, v unchanged).
+__device__ inline bool peer_allreduce_wave(const PeerArgs& a, double* v, int nsum, int nv) {
+  const int lane = threadIdx.x & 63;
+  const int par = int(a.tag & 1);
+  for (int t = lane; t < nv; t += 64) {
+    const double x = v[t];
+    for (int q = 0; q < a.P; ++q) red_slot(a.base[q], a.P, par, a.rank)[t] = x;
+  }
+  __threadfence_system();
+  __builtin_amdgcn_wave_barrier();
+  for (int q = lane; q < a.P; q += 64)
+    __hip_atomic_store(red_flag(a.base[q], par, a.rank), a.tag, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = true;
+  for (int q = lane; q < a.P; q += 64) ok = ok && wait_tag(a, red_flag(a.base[a.rank], par, q));
+  // every lane's waits, combined (a lane with no peer to wait for reports ok)
+  if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
+  __threadfence_system();
+  char* mine = a.base[a.rank];
+  for (int t = lane; t < nv; t += 64) {
+    double acc = red_slot(mine, a.P, par, 0)[t];
+    for (int q = 1; q < a.P; ++q) {
+      const double x = red_slot(mine, a.P, par, q)[t];
+      acc = (t < nsum) ? acc + x : nmax(acc, x);
+    }
+    v[t] = acc;
+  }
+  return true;
+}
+
+}  // namespace nk

@@ -4,6 +4,8 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "peer_dev.h"
+
 namespace nk {
 
 // ============================================================================================
@@ -337,13 +339,23 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   }
   // edge rows of u -> the ring neighbours (y4_ holds rows 0, 1, ny-2, ny-1 as a 4-row slab)
   const double eb = 8.0 * 4 * nx_ * (z ? 2 : nv + 2);
-  int rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
-  if (rc) return rc;
-  rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
-    return E_.comm->halo(y4_, yh_, yh_ + 2 * nx_, 4, nx_, E_.s) == NK_OK ? hipSuccess
-                                                                       : hipErrorUnknown;
-  });
-  if (rc) return NK_ECOMM;
+  int rc = NK_OK;
+  PeerArgs pa;
+  if (!split && peer_fuse_enabled() && E_.comm->take_halo(&pa, nx_)) {
+    // peer-memory communicator: the edge rows go straight into the neighbours' staging rows
+    // and come back into yh_ in the same launch (no y4_ round trip, no separate halo kernel)
+    rc = E_.launch(K_ARN_EDGE, eb + 2.0 * 4 * 8 * nx_,
+                   [&] { return arnoldi_edge_halo_launch(A, pa, yh_, E_.s); });
+    if (rc) return rc;
+  } else {
+    rc = E_.launch(K_ARN_EDGE, eb, [&] { return arnoldi_edge_launch(A, y4_, E_.s); });
+    if (rc) return rc;
+    rc = E_.launch(K_HALO, 2.0 * 4 * 8 * nx_, [&] {
+      return E_.comm->halo(y4_, yh_, yh_ + 2 * nx_, 4, nx_, E_.s) == NK_OK ? hipSuccess
+                                                                         : hipErrorUnknown;
+    });
+    if (rc) return NK_ECOMM;
+  }
   if (!split) {
     A.yh = yh_;
     return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });

@@ -1,19 +1,21 @@
 #!/bin/bash
 # World-size-1 cost of the slab path: plain periodic slab vs the peer-memory communicator vs
-# RCCL (bench.py --peer-self / --rccl-self), alternating inside one gpurun call.
+# RCCL (bench.py --peer-self / --rccl-self), alternating inside one gpurun call (VARIANTS=...).
 #   bash scripts/ab_comm.sh [rounds]
 set -u
 R=${1:-2}
 ARGS="--steps 10 --warmup 2 --extra off --cpu-baseline off"
 mkdir -p gpurun_out
 for i in $(seq 1 "$R"); do
-  for V in plain peer rccl; do
+  for V in ${VARIANTS:-plain peer peer0 rccl}; do
+    F=1
     case $V in
       plain) X="" ;;
-      peer) X="--peer-self" ;;
+      peer) X="--peer-self" ;;  # collectives inside the edge / reduction-control kernels
+      peer0) X="--peer-self"; F=0 ;;  # separate communicator launches (NKHIP_PEER_FUSE=0)
       rccl) X="--rccl-self" ;;
     esac
-    timeout -k 10 300 python3 bench.py $ARGS $X > gpurun_out/abc_${V}_$i.log 2>&1 || { echo "$V failed"; tail -5 gpurun_out/abc_${V}_$i.log; exit 1; }
+    NKHIP_PEER_FUSE=$F timeout -k 10 300 python3 bench.py $ARGS $X > gpurun_out/abc_${V}_$i.log 2>&1 || { echo "$V failed"; tail -5 gpurun_out/abc_${V}_$i.log; exit 1; }
     python3 - "$V" gpurun_out/abc_${V}_$i.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

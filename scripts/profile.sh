@@ -24,5 +24,6 @@ run write 600 --pmc WRITE_SIZE
 cmp -s "$OUT/trace.launches" "$OUT/fetch.launches" && cmp -s "$OUT/trace.launches" "$OUT/write.launches" \
   && echo "launch logs identical" || echo "WARNING: launch logs differ between passes"
 python3 scripts/traffic_match.py "$TAG" "$OUT" "$OUT/trace.launches" > "$OUT/traffic_match.log" 2>&1
+cp profiles/${TAG}_traffic.json "$OUT/" 2>/dev/null || true
 echo "traffic_match rc=$?"
 find "$OUT" -name "*.csv" | head -20

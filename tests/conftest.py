@@ -58,3 +58,19 @@ def run_slabs(comms, body, timeout=300):
         c.close()
     if errs:
         raise errs[0]
+
+
+@pytest.fixture(autouse=True)
+def _bounds_check():
+    """Under the bounds-checked library (NKHIP_BOUNDS=1 with NKHIP_LIB=.../libnkhip_check.so,
+    tests/test_gpu_bounds.py): fail the test whose kernels computed an out-of-range index."""
+    yield
+    if os.environ.get("NKHIP_BOUNDS") != "1" or "nkhip" not in sys.modules:
+        return
+    import ctypes as C
+
+    from nkhip import _lib
+    n, line = C.c_int64(0), C.c_int32(0)
+    rc = _lib.lib.nk_debug_bounds(C.byref(n), C.byref(line), 1)
+    assert rc == 0, f"nk_debug_bounds rc={rc} (not the bounds-checked library?)"
+    assert n.value == 0, f"{n.value} out-of-range indices, first at arnoldi.hip:{line.value}"

@@ -1,0 +1,36 @@
+"""GPU: the fused Arnoldi and slab-edge kernels never index outside their arrays.
+
+GPU AddressSanitizer is not available on this pool, so `make check` builds the same C-ABI with
+every index the fused kernels compute checked in the kernel (arnoldi.hip CI()/ARN_CHK(): the row
+and column of each streamed load, the block-halo and edge-array offsets, the slab halo rows, the
+mailbox records, the store offsets and the partial-sum slots).  An out-of-range index is counted
+and replaced by 0 instead of faulting.  This test runs the fused-kernel test module against that
+library in one child process; conftest.py's autouse fixture reads the counters after every test
+and fails the test whose launches computed a bad index.  The module covers partial last blocks
+(nx = 600, 130, 40), the smallest grids, every basis length, edge arrays on and off, the mailbox
+in all three modes, augmentation steps, and 2/3/4/8 loopback row slabs (serial and split).
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHECK_LIB = os.path.join(ROOT, "iterative-solvers-summer-2020_amd", "nkhip", "libnkhip_check.so")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(900)
+def test_fused_kernels_stay_in_bounds():
+    assert os.path.exists(CHECK_LIB), "build it: make -C iterative-solvers-summer-2020_amd check"
+    env = dict(os.environ, NKHIP_LIB=CHECK_LIB, NKHIP_BOUNDS="1")
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "tests/test_gpu_fused.py", "-x", "-q",
+                        "-m", "gpu", "-p", "no:cacheprovider", "--timeout", "300",
+                        "--timeout-method", "thread"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=880)
+    tail = "\n".join((r.stdout + r.stderr).splitlines()[-25:])
+    print(tail)
+    assert r.returncode == 0, tail
+    assert " passed" in r.stdout and "failed" not in r.stdout, tail
