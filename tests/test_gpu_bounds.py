@@ -8,7 +8,8 @@ and replaced by 0 instead of faulting.  This test runs the fused-kernel test mod
 library in one child process; conftest.py's autouse fixture reads the counters after every test
 and fails the test whose launches computed a bad index.  The module covers partial last blocks
 (nx = 600, 130, 40), the smallest grids, every basis length, edge arrays on and off, the mailbox
-in all three modes, augmentation steps, and 2/3/4/8 loopback row slabs (serial and split).
+in all three modes, augmentation steps, and 2/3/4/8 loopback row slabs (serial and split); the
+world-of-one peer-memory slab adds the edge kernel that runs the halo exchange itself.
 """
 import os
 import subprocess
@@ -26,7 +27,8 @@ pytestmark = pytest.mark.gpu
 def test_fused_kernels_stay_in_bounds():
     assert os.path.exists(CHECK_LIB), "build it: make -C iterative-solvers-summer-2020_amd check"
     env = dict(os.environ, NKHIP_LIB=CHECK_LIB, NKHIP_BOUNDS="1")
-    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "tests/test_gpu_fused.py", "-x", "-q",
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "tests/test_gpu_fused.py",
+                        "tests/test_gpu_peer.py::test_peer_world1_matches_single_slab", "-x", "-q",
                         "-m", "gpu", "-p", "no:cacheprovider", "--timeout", "300",
                         "--timeout-method", "thread"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=880)
