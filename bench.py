@@ -10,10 +10,13 @@ U0 = default_rng(2020).standard_normal(N^2), scipy-default tolerances, FD (scipy
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-N > 1: the same 4096^2 grid is cut into N row slabs (strong scaling), RCCL halo + all-reduce.
+N > 1: the same 4096^2 grid is cut into N row slabs (strong scaling); halo exchange and
+all-reduce through the peer-memory communicator over xGMI (default) or RCCL (--comm rccl).
 value = time steps per second of the whole job (max over ranks of the timed region).
 Rank 0 prints ONE JSON line.  The kernel roofline comes from HIP events recorded around every
-kernel on the solver's stream inside the timed region (nk_sh_kernel_profile).
+kernel on the solver's stream inside the timed region (nk_sh_kernel_profile); roofline.traffic
+from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this bench on
+the same box after the timed region (N=1; --pmc off: the last committed profile's ratios).
 """
 from __future__ import annotations
 
@@ -48,7 +51,59 @@ def parse():
                     help="testing: build the peer-memory communicator even at world size 1")
     ap.add_argument("--extra", choices=["on", "off"], default="on",
                     help="also measure configs 2 (1024^2 Lap SpMV) and 3 (91x61 droplet)")
+    ap.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                    help="HBM traffic of this box: two rocprofv3 --pmc passes (FETCH_SIZE, "
+                         "WRITE_SIZE) over a short child run of this bench, N=1 only")
+    ap.add_argument("--probes", choices=["on", "off"], default="on",
+                    help="the isolated-JVP and copy-bandwidth probes after the timed region")
     return ap.parse_args()
+
+
+def pmc_traffic(args):
+    """roofline.traffic measured on THIS box in THIS run: the bench itself, 1 warmup + 1 timed
+    step at the same grid, run twice as a child process under rocprofv3 -- one --pmc FETCH_SIZE
+    pass and one --pmc WRITE_SIZE pass (separate passes, MI355X_MICROARCH.md: read bytes =
+    2 x FETCH_SIZE KiB, write bytes = WRITE_SIZE KiB on gfx950) -- each with the solver's launch
+    log, matched dispatch by dispatch (scripts/traffic_match.py).  None when rocprofv3 is absent
+    or a pass fails (the line then falls back to profiles/latest_traffic.json)."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    d = tempfile.mkdtemp(prefix="nkhip_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1",
+             "--n", str(args.n), "--jvp", args.jvp, "--extra", "off", "--cpu-baseline", "off",
+             "--pmc", "off", "--probes", "off"]
+    t0 = time.perf_counter()
+    try:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            env = dict(os.environ, NKHIP_LAUNCH_LOG=os.path.join(d, c + ".launches"),
+                       TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+            r = subprocess.run([prof, "--pmc", c, "-d", os.path.join(d, c), "-o", c,
+                                "--output-format", "csv", "--"] + child, env=env,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150)
+            if r.returncode != 0:
+                return None
+        logs = [open(os.path.join(d, c + ".launches")).read() for c in ("FETCH_SIZE", "WRITE_SIZE")]
+        if logs[0] != logs[1]:  # the two passes must be the same deterministic program
+            return None
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import traffic_match as tm
+        res = tm.match(tm.find(os.path.join(d, "FETCH_SIZE"), "counter_collection.csv"),
+                       tm.find(os.path.join(d, "WRITE_SIZE"), "counter_collection.csv"), None,
+                       os.path.join(d, "FETCH_SIZE.launches"), "bench")
+        res["source"] = ("this run, this box: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE "
+                         "passes over a child run of this bench (1 warmup + 1 step, same grid), "
+                         "matched dispatch by dispatch to the solver's launch log; HBM bytes = "
+                         "2 x FETCH_SIZE KiB + WRITE_SIZE KiB (gfx950)")
+        res["seconds"] = round(time.perf_counter() - t0, 1)
+        return res
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def cpu_baseline(n, h, k, r, g, u_start, gpu_fevals_per_step):
@@ -425,7 +480,9 @@ def main():
             v["ms_est"] = v["ms"] * v["launches"] / v["timed"]
         dom = max(ker, key=lambda k_: ker[k_]["ms_est"]) if ker else None
 
-        traffic_db = load_traffic()
+        # PMC traffic of this run (two child passes under rocprofv3), else the last profile's
+        live = pmc_traffic(args) if (world == 1 and args.pmc == "auto") else None
+        traffic_db = live or load_traffic()
 
         def roof(name):
             v = ker[name]
@@ -490,17 +547,24 @@ def main():
             "final_step_check": final_check,
             "cpu_baseline": None,
         }
-        if world == 1:
-            out["jvp_roofline_isolated"] = jvp_isolated(n, h, r, k, g, a, args.jvp)
-        # the box's measured streaming rate beside the 8 TB/s spec: frac_of_measured makes the
-        # fractions comparable across boxes
-        cb = copy_bandwidth(n)
-        out["copy_bandwidth"] = cb
-        for key in ("roofline", "jvp_roofline", "jvp_roofline_isolated"):
-            rl = out.get(key)
-            if rl:
-                rl["peak_measured"] = cb["GB/s"]
-                rl["frac_of_measured"] = round(rl["achieved"] / cb["GB/s"], 4)
+        out["traffic_measurement"] = (
+            {"live": True, "seconds": live.get("seconds"),
+             "classes": {c: round(v["traffic_over_alg"], 4) for c, v in live["classes"].items()
+                         if v.get("traffic_over_alg")}}
+            if live else {"live": False, "file": "profiles/latest_traffic.json",
+                          "tag": traffic_db.get("tag")})
+        if args.probes == "on":
+            if world == 1:
+                out["jvp_roofline_isolated"] = jvp_isolated(n, h, r, k, g, a, args.jvp)
+            # the box's measured streaming rate beside the 8 TB/s spec: frac_of_measured makes
+            # the fractions comparable across boxes
+            cb = copy_bandwidth(n)
+            out["copy_bandwidth"] = cb
+            for key in ("roofline", "jvp_roofline", "jvp_roofline_isolated"):
+                rl = out.get(key)
+                if rl:
+                    rl["peak_measured"] = cb["GB/s"]
+                    rl["frac_of_measured"] = round(rl["achieved"] / cb["GB/s"], 4)
         if want_cpu:
             fe = (tot["nfev"] + tot["njvp"]) / args.steps
             rec, u_cpu = cpu_baseline(n, h, k, r, g, u_start, fe)

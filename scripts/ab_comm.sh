@@ -4,7 +4,7 @@
 #   bash scripts/ab_comm.sh [rounds]
 set -u
 R=${1:-2}
-ARGS="--steps 10 --warmup 2 --extra off --cpu-baseline off"
+ARGS="--steps 10 --warmup 2 --extra off --cpu-baseline off --pmc off"
 mkdir -p gpurun_out
 for i in $(seq 1 "$R"); do
   for V in ${VARIANTS:-plain peer peer0 rccl}; do

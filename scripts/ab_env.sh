@@ -4,7 +4,7 @@
 # e.g. bash scripts/ab_env.sh 2 "NKHIP_PF=1" "NKHIP_PF=2".  BENCH_ARGS overrides the bench args.
 set -u
 R=$1; shift
-ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --extra off --cpu-baseline off"}
+ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --extra off --cpu-baseline off --pmc off"}
 mkdir -p gpurun_out
 for i in $(seq 1 "$R"); do
   k=0

@@ -4,7 +4,7 @@
 # [bench args...].  Prints steps/s, the dominant-kernel and JVP fractions and the box's copy rate.
 set -u
 A=$1; B=$2; R=${3:-2}; shift 3 || shift $#
-ARGS=${*:-"--steps 10 --warmup 2 --extra off --cpu-baseline off"}
+ARGS=${*:-"--steps 10 --warmup 2 --extra off --cpu-baseline off --pmc off"}
 mkdir -p gpurun_out
 for i in $(seq 1 "$R"); do
   for L in "$A" "$B"; do

@@ -4,7 +4,7 @@
 # Usage on the GPU box: bash scripts/profile.sh <tag> [bench args...]
 set -u
 TAG=${1:-r02}; shift || true
-ARGS=${*:-"--steps 3 --warmup 1 --cpu-baseline off --extra off"}
+ARGS=${*:-"--steps 3 --warmup 1 --cpu-baseline off --extra off --pmc off"}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

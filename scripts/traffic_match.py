@@ -79,17 +79,16 @@ def by_class(disp):
     return q
 
 
-def main():
-    tag, prof, logf = sys.argv[1], sys.argv[2], sys.argv[3]
+def match(fetch_csv, write_csv, trace_csv, launch_log, tag):
+    """Per-class traffic of the dispatches in the FETCH_SIZE / WRITE_SIZE counter CSVs matched to
+    the launch log (trace_csv, optional: per-dispatch durations)."""
     log = collections.defaultdict(list)
-    for line in open(logf):
+    for line in open(launch_log):
         c, b = line.split()
         log[c].append(float(b))
-    fetch = by_class(per_dispatch(find(os.path.join(prof, "fetch"), "counter_collection.csv"),
-                                  "FETCH_SIZE"))
-    write = by_class(per_dispatch(find(os.path.join(prof, "write"), "counter_collection.csv"),
-                                  "WRITE_SIZE"))
-    trace = by_class(per_dispatch(find(os.path.join(prof, "trace"), "kernel_trace.csv")))
+    fetch = by_class(per_dispatch(fetch_csv, "FETCH_SIZE"))
+    write = by_class(per_dispatch(write_csv, "WRITE_SIZE"))
+    trace = by_class(per_dispatch(trace_csv)) if trace_csv else {}
     res = {"tag": tag, "source": ("per-dispatch match of rocprofv3 FETCH_SIZE / WRITE_SIZE / "
                                   "kernel-trace passes to the solver's launch log "
                                   "(scripts/traffic_match.py)"), "classes": {}}
@@ -109,10 +108,18 @@ def main():
                "alg_bytes_per_launch": sum(alg) / n,
                "hbm_bytes_per_launch": (sum(rd) + sum(wr)) / n}
         dur = trace.get(c, [])[:n]
-        if len(dur) == n:
+        if dur and len(dur) == n:
             rec["avg_us"] = sum(dur) / n / 1e3
             rec["alg_GBps"] = sum(alg) / sum(dur)  # bytes per ns = GB/s
         res["classes"][c] = rec
+    return res
+
+
+def main():
+    tag, prof, logf = sys.argv[1], sys.argv[2], sys.argv[3]
+    res = match(find(os.path.join(prof, "fetch"), "counter_collection.csv"),
+                find(os.path.join(prof, "write"), "counter_collection.csv"),
+                find(os.path.join(prof, "trace"), "kernel_trace.csv"), logf, tag)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     for name in (f"{tag}_traffic.json", "latest_traffic.json"):
         json.dump(res, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
