@@ -378,6 +378,29 @@ def copy_bandwidth(n, reps=20):
                     "after the timed region"}
 
 
+def peer_or_rccl(nkhip, dist, torch, max_nx):
+    """The peer-memory communicator, verified before it is used: one all-reduce and one halo
+    exchange of known values through it (nk_comm_selftest; device waits are bounded).  If any
+    rank cannot create, map or verify it, every rank falls back to RCCL (stderr says so)."""
+    comm, ok = None, 1
+    try:
+        comm = nkhip.PeerComm.from_torch_distributed(max_nx=max_nx)
+        ok = int(comm.selftest(min(max_nx, 4096)))
+    except Exception as e:  # noqa: BLE001 - any failure means: use RCCL instead
+        print(f"peer-memory communicator unavailable: {e}", file=sys.stderr)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return comm
+    print("peer-memory communicator failed its self-test on some rank: using RCCL",
+          file=sys.stderr)
+    if comm is not None:
+        comm.abort()
+        comm.close()
+    return nkhip.RcclComm.from_torch_distributed()
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "latest_traffic.json")
     try:
@@ -415,7 +438,7 @@ def main():
         if args.rccl_self or (world > 1 and args.comm == "rccl" and not args.peer_self):
             comm = nkhip.RcclComm.from_torch_distributed()
         else:
-            comm = nkhip.PeerComm.from_torch_distributed(max_nx=args.n)
+            comm = peer_or_rccl(nkhip, dist, torch, args.n)
 
     n = args.n
     h, k, r, g = 0.625, 0.2, 0.01, 1.0

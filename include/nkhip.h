@@ -213,6 +213,10 @@ int nk_comm_destroy(nk_comm* c);
  * released by the launcher's own failure handling (e.g. the torch.distributed watchdog).  A stepper calls it itself when one of its steps fails with a negative code; a host
  * thread that fails outside the library calls it before it exits. */
 int nk_comm_abort(nk_comm* c);
+/* One all-reduce (sums and maxima) and one halo exchange of known values through the group,
+ * checked on the host; every rank calls it (a collective).  NK_OK, or NK_ECOMM when a value did
+ * not arrive intact (bench.py falls back from the peer-memory communicator to RCCL on that). */
+int nk_comm_selftest(nk_comm* c, int64_t nx, void* stream);
 
 /* ---------------- Swift-Hohenberg implicit time step (the north-star path) ---------------- */
 /* A stepper for one row slab [row0, row0+ny_local) of an ny_global x nx periodic grid.

@@ -391,6 +391,50 @@ int nk_comm_abort(nk_comm* c) {
   return NK_OK;
 }
 
+// One all-reduce and one halo exchange of known values through the communicator, checked on the
+// host: every rank contributes (rank + 1 + i) to the sums and (rank + i) to the maxima, and a
+// 4-row slab whose entries encode (rank, row, column).
+int nk_comm_selftest(nk_comm* c, int64_t nx, void* stream) {
+  if (!c || nx < 1) return NK_EINVAL;
+  const hipStream_t s = S(stream);
+  const int P = c->size(), r = c->rank();
+  constexpr int kV = 8, kSum = 5;
+  const int64_t nslab = 4 * nx, nhalo = 4 * nx;
+  std::vector<double> h(kV + nslab + nhalo);
+  for (int i = 0; i < kV; ++i) h[i] = (i < kSum) ? r + 1.0 + i : r + double(i);
+  auto code = [&](int q, int64_t row, int64_t j) { return 1e6 * q + double(row * nx + j); };
+  for (int64_t row = 0; row < 4; ++row)
+    for (int64_t j = 0; j < nx; ++j) h[kV + row * nx + j] = code(r, row, j);
+  double* d = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&d), h.size() * sizeof(double)) != hipSuccess)
+    return NK_EHIP;
+  int rc = hipMemcpyAsync(d, h.data(), (kV + nslab) * sizeof(double), hipMemcpyHostToDevice, s) ==
+                   hipSuccess
+               ? NK_OK
+               : NK_EHIP;
+  if (!rc) rc = c->allreduce(d, kSum, kV, s);
+  if (!rc) rc = c->halo(d + kV, d + kV + nslab, d + kV + nslab + 2 * nx, 4, nx, s);
+  if (!rc && (hipMemcpyAsync(h.data(), d, h.size() * sizeof(double), hipMemcpyDeviceToHost, s) !=
+                  hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+    rc = NK_EHIP;
+  (void)hipFree(d);
+  if (rc) return rc;
+  if (c->failed()) return NK_ECOMM;
+  for (int i = 0; i < kV; ++i) {
+    const double want = (i < kSum) ? P * (P + 1) / 2.0 + double(P) * i : (P - 1.0) + i;
+    if (h[i] != want) return NK_ECOMM;
+  }
+  const int prev = (r - 1 + P) % P, next = (r + 1) % P;
+  const double* lo = h.data() + kV + nslab;
+  const double* hi = lo + 2 * nx;
+  for (int64_t row = 0; row < 2; ++row)
+    for (int64_t j = 0; j < nx; ++j)
+      if (lo[row * nx + j] != code(prev, 2 + row, j) || hi[row * nx + j] != code(next, row, j))
+        return NK_ECOMM;
+  return NK_OK;
+}
+
 // ------------------------------------------------------------------------------ SH stepper
 int nk_sh_create(nk_sh** out, int64_t ny_local, int64_t nx, int64_t ny_global, double h, double r,
                  double k, double g, const nk_opts* opts, nk_comm* comm, void* stream) {

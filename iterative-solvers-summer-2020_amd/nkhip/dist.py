@@ -54,6 +54,14 @@ class Comm:
             lib.nk_comm_destroy(self.handle)
             self.handle = None
 
+    def selftest(self, nx: int = 64) -> bool:
+        """A collective (every rank calls it): one all-reduce and one halo exchange of known
+        values through the group, checked on the host (nk_comm_selftest).  False: a value did
+        not arrive intact or a wait gave up."""
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+        return lib.nk_comm_selftest(self.handle, int(nx), C.c_void_p(stream)) == 0
+
 
 class RcclComm(Comm):
     @staticmethod

@@ -42,6 +42,7 @@ def test_peer_world1_matches_single_slab():
     ref = _single(N, U0)
     (comm,) = nkhip.peer_comms(1, N)
     try:
+        assert comm.selftest(N)
         m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comm, ny_local=N)
         got = m.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
         m.close()
@@ -99,6 +100,7 @@ rank, world, N = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), int(os.
 torch.cuda.set_device(0)
 dist.init_process_group("gloo")
 comm = nkhip.PeerComm.from_torch_distributed(max_nx=N)
+assert comm.selftest(N), "nk_comm_selftest failed"  # the bench's check before it trusts the group
 U0 = np.random.default_rng(2020).standard_normal((N, N))
 row0, ny = nkhip.slab_rows(N, rank, world)
 m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comm, ny_local=ny)
