@@ -254,6 +254,92 @@ __device__ __forceinline__ double dpp_down(double x) {
   return __builtin_bit_cast(double, r);
 }
 
+// u = v (or z) at element o of the grid, summed in the fused kernel's order -- for the pair
+// layout (h0 = 0) entries 0, 2, 4, .. of [V_0 .. V_{nv-1}, w] in one partial, 1, 3, 5, .. in the
+// other, then their sum; for the wide layout (h0 = nv + 1) all entries in order -- so an edge row
+// sent to a neighbour equals the row its owner computes.  Every entry load is in flight at once.
+template <int NV>
+__device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0, double a_tau) {
+  if (A.z) return A.z[o];
+  constexpr int NE = NV + 1;
+  double x[NE], cf[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    x[e] = ((e < NV) ? A.V[e] : A.w)[o];
+    cf[e] = (e < NV) ? arn_c(A, e) : a_tau;
+  }
+  double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    if ((h0 > 0) ? (e < h0) : ((e & 1) == 0))
+      p0 = __builtin_fma(cf[e], x[e], p0);
+    else
+      p1 = __builtin_fma(cf[e], x[e], p1);
+  }
+  return p0 + p1;
+}
+
+// ------------------------------------------------------------------------------------------
+// Slab exchange inside the fused kernel (row slabs over the peer-memory communicator, A.x.me set;
+// peer_dev.h holds the buffer layout).  A slab's stencil needs u on the neighbours' two edge rows,
+// and u of a row needs only the basis, not the stencil: so the blocks of the FIRST band compute u
+// on the slab's rows 0, 1 for their own columns and write it straight into the previous rank's
+// "hi" staging rows, the blocks of the LAST band do the same with rows ny-2, ny-1 into the next
+// rank's "lo" rows; each then publishes one flag per 128-column chunk it wrote (tagged, release,
+// system scope) and waits for the chunks its own halo columns need in its own buffer (its
+// columns plus two either side) before its march starts.  Publishing never waits, so there is no
+// cycle; the interior bands (all but two per column group) never wait at all, which is the
+// overlap: the exchange runs beside the interior of the pass instead of before it (the edge
+// kernel + halo kernel in series, ~22 us per Arnoldi step).  The halo rows are then read from
+// this rank's staging rows (A.yh, row stride A.yh_ld).  A wait that gives up (abort, ~20 s) sets
+// the communicator's error word; the host sees it at its next synchronisation.
+template <int NV>
+__device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW, int h0,
+                                double a_tau) {
+  const SlabX& X = A.x;
+  const int64_t nx = A.nx, ny = A.ny;
+  const bool first = band == 0, last = band == int64_t(A.nbands) - 1;
+  const int par = int(X.tag & 1);
+  const int64_t cend = (B0 + BW < nx) ? B0 + BW : nx;  // own columns [B0, cend)
+  for (int side = 0; side < 2; ++side) {  // side 0: my rows 0, 1 -> prev; 1: ny-2, ny-1 -> next
+    if (side == 0 ? !first : !last) continue;
+    char* dst = side == 0 ? X.prev : X.next;
+    const int dside = side == 0 ? 1 : 0;  // the receiver's "hi" / "lo" staging rows
+    for (int rr = 0; rr < 2; ++rr) {
+      const int64_t row = side == 0 ? rr : ny - 2 + rr;
+      for (int64_t j = B0 + threadIdx.x; j < cend; j += blockDim.x) {
+        ARN_CHK(j < X.max_nx && row * nx + j < ny * nx);
+        stage(dst, X.P, X.max_nx, par, dside, rr)[j] = edge_u<NV>(A, row * nx + j, h0, a_tau);
+      }
+    }
+    __threadfence_system();
+    __syncthreads();
+    // one flag per chunk this block wrote (B0 and BW are multiples of kXChunk)
+    for (int64_t ch = B0 / kXChunk + threadIdx.x; ch * kXChunk < cend; ch += blockDim.x) {
+      ARN_CHK(ch < x_chunks(X.max_nx));
+      __hip_atomic_store(xflag(dst, X.P, X.max_nx, par, dside, ch), X.tag, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // the chunks my halo columns come from, in my buffer: side 0 ("lo", from prev) for the first
+  // band, side 1 ("hi", from next) for the last; chunks of columns B0-2, [B0, cend), B0+BW
+  const int64_t nch = (nx + kXChunk - 1) / kXChunk;
+  const int64_t cl = ((B0 - 2 + nx) % nx) / kXChunk, c0 = B0 / kXChunk;
+  const int64_t c1 = (cend - 1) / kXChunk, cr = ((B0 + BW) % nx) / kXChunk;
+  const int64_t nown = c1 - c0 + 1;
+  for (int side = 0; side < 2; ++side) {
+    if (side == 0 ? !first : !last) continue;
+    const int t = int(threadIdx.x);
+    if (t < nown + 2) {
+      const int64_t ch = (t == 0) ? cl : ((t == 1) ? cr : c0 + (t - 2));
+      ARN_CHK(ch >= 0 && ch < nch);
+      (void)wait_flag_tag(xflag(X.me, X.P, X.max_nx, par, side, ch), X.tag, X.me, X.err);
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the staged rows, for every thread of the block
+}
+
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
 //   [V_0 .. V_{NV-1}, w, x0, (z)]
@@ -376,6 +462,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   // and the x0 halo lanes read it there in place of x0)
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
+  const int64_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
 
   auto wrap = [&](int64_t q) -> int64_t {
     q = (q > r1 + 1) ? r1 + 1 : q;  // past the band halo: re-read its last row
@@ -467,7 +554,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
     const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
-    const int64_t yo = CI(hq * nx + col, 4 * nx - 1);
+    const int64_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const double* a = ep[k] + o;
@@ -482,9 +569,9 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       s.hv = gld(useE ? hE + eo : hp + ho);
     }
     // z on the halo columns (EXT, lanes 4..); u of a slab halo row (A.yh, lanes 0-3); every
-    // other lane one fixed line
-    const int64_t hyo = CI(hq * nx + hcol, 4 * nx);
-    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? yhb : hxp + ho));
+    // other lane one fixed line of x0 (not of A.yh: the halo rows may sit in uncached peer memory)
+    const int64_t hyo = CI(hq * yld + hcol, 4 * yld);
+    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? A.x0 : hxp + ho));
     s.own = !hrow;
   };
   // entry e of this row for both halves (e is a compile-time index)
@@ -674,6 +761,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     h2q.y = h2q.y + h.y;
   };
 
+  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
     // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
@@ -849,6 +937,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
+  const int64_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
   auto wrap = [&](int64_t q) -> int64_t {
     q = (q > r1 + 1) ? r1 + 1 : q;
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
@@ -925,7 +1014,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
     const bool hrow = halo_row(q);
     const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
-    const int64_t yo = CI(hq * nx + col, 4 * nx - 1);
+    const int64_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const double* a = src(e) + o;
@@ -937,8 +1026,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
       const int64_t eo = CI(useE ? ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh : 0, eelem);
       s.hv = gld(useE ? hE + eo : hp + ho);
     }
-    const int64_t hyo = CI(hq * nx + hcol, 4 * nx);
-    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? yhb : hxp + ho));
+    const int64_t hyo = CI(hq * yld + hcol, 4 * yld);
+    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? A.x0 : hxp + ho));
     s.own = !hrow;
   };
   auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
@@ -1091,6 +1180,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     h2q.y = h2q.y + h.y;
   };
 
+  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau);  // uniform per block
   if (nrows > 0) {
     Slot P[2];
     load(P[0], r0 - 2);
@@ -1327,31 +1417,9 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
   const int t = blockIdx.y;
   const int64_t row = (t < 2) ? t : A.ny - 4 + t;
   const int64_t o = CI(row * A.nx + (j < A.nx ? j : 0), A.ny * A.nx);
-  double y;  // the stencil input u of the fused kernel
-  if (A.z) {
-    y = A.z[o];
-  } else {
-    // every entry of [V_0 .. V_{nv-1}, w] and its coefficient in flight at once (the kernel is
-    // latency-bound: 4 rows of a slab -- batches of 8 took 10 us per launch); the sums then run
-    // in entry order within each partial
-    constexpr int NE = NV + 1;
-    double x[NE], cf[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      x[e] = ((e < NV) ? A.V[e] : A.w)[o];
-      cf[e] = (e < NV) ? arn_c(A, e) : a_tau;
-    }
-    double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      // wide layout (h0 = nv + 1): all in p0; vector pairs (h0 = 0): even entries in p0
-      if ((h0 > 0) ? (e < h0) : ((e & 1) == 0))
-        p0 = __builtin_fma(cf[e], x[e], p0);
-      else
-        p1 = __builtin_fma(cf[e], x[e], p1);
-    }
-    y = p0 + p1;
-  }
+  // the stencil input u of the fused kernel (the kernel is latency-bound: 4 rows of a slab --
+  // every entry load in flight at once; batches of 8 took 10 us per launch)
+  const double y = edge_u<NV>(A, o, h0, a_tau);
   if constexpr (!PEER) {
     y4[int64_t(t) * A.nx + j] = y;
   } else {

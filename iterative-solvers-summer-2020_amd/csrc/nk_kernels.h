@@ -10,6 +10,8 @@
 
 #include <cstdint>
 
+struct nk_comm;  // comm.h
+
 namespace nk {
 
 struct PeerArgs;  // peer_dev.h (the peer-memory communicator's device-side arguments)
@@ -17,6 +19,10 @@ struct PeerArgs;  // peer_dev.h (the peer-memory communicator's device-side argu
 // them (arnoldi_edge_halo_launch, arn_reduce_allreduce_ctl_launch); NKHIP_PEER_FUSE=0 (read per
 // call) keeps the separate communicator launches.
 bool peer_fuse_enabled();
+// The fused kernel runs the slab exchange itself (arnoldi.hip "Slab exchange"), with the peer
+// communicator (and NKHIP_PEER_FUSE on): NKHIP_SLAB_XK=2 when the ranks do not share a GPU, 1
+// always (tests: several processes on one GPU); unset / 0: off (read per call).
+bool slab_x_enabled(const nk_comm* c);
 
 // ---------------------------------------------------------------------------------------------
 struct Field {
@@ -139,6 +145,18 @@ constexpr int kEdgeW = 256;
 __host__ __device__ inline int64_t edge_groups(int64_t nx) { return (nx + kEdgeW - 1) / kEdgeW; }
 __host__ __device__ inline int64_t edge_elems(int64_t ny, int64_t nx) { return edge_groups(nx) * ny * 4; }
 hipError_t edge_gather_launch(const double* v, double* E, int64_t ny, int64_t nx, hipStream_t s);
+// In-kernel slab exchange over the peer-memory communicator (arnoldi.hip "Slab exchange"): the
+// fused kernel's edge bands publish u on the slab's edge rows straight into the neighbours'
+// staging rows and wait for theirs; me == nullptr: off.
+struct SlabX {
+  char* me = nullptr;  // this rank's peer buffer, and the ring neighbours' (peer_dev.h layout)
+  char* prev = nullptr;
+  char* next = nullptr;
+  int P = 0;
+  int64_t max_nx = 0;
+  uint64_t tag = 0;
+  int* err = nullptr;  // pinned host error word of the communicator
+};
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;
   int nv = 0;                      // basis vectors V_0..V_{nv-1}
@@ -163,6 +181,8 @@ struct ArnoldiArgs {
   // row slab (one of several): u on the halo rows -2, -1, ny, ny+1 (4 rows of nx, filled by
   // arnoldi_edge_launch on every rank + the halo exchange); nullptr = single periodic slab
   const double* yh = nullptr;
+  int64_t yh_ld = 0;               // row stride of yh (0: nx)
+  SlabX x{};                       // in-kernel slab exchange (yh = this rank's staging rows)
   double* partial = nullptr;       // [(2 nv + 3)][pstride], this launch's columns from pcol0
   int64_t partial_cap = 0;         // doubles available at partial
   // rows [r_begin, r_end) of the slab are computed (r_end < 0: ny); rows outside are read only

@@ -202,6 +202,12 @@ bool peer_fuse_enabled() {
   return !(e && e[0] == '0');
 }
 
+bool slab_x_enabled(const nk_comm* c) {
+  const char* e = std::getenv("NKHIP_SLAB_XK");
+  if (!(e && (e[0] == '1' || e[0] == '2')) || !c || !peer_fuse_enabled()) return false;
+  return e[0] == '1' || !c->shares_device();
+}
+
 int comm_peer_handle_bytes() { return int(sizeof(PeerBlob)); }
 
 int comm_create_peer(nk_comm** out, int rank, int nranks, int64_t max_nx, void* handle_out) {

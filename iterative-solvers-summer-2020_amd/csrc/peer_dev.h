@@ -23,8 +23,15 @@ constexpr int64_t kOffRedSlot = 2048;                             // [2][P][kRed
 __host__ __device__ inline int64_t off_stage(int P) {             // [2][2][2][max_nx] double
   return (kOffRedSlot + int64_t(2) * P * kRedMax * 8 + 255) / 256 * 256;
 }
-__host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
+// chunk flags of the in-kernel slab exchange (arnoldi.hip, "Slab exchange"): [2][2][chunks] uint64
+// after the staging rows, one per parity, side and kXChunk-column chunk of a staged row pair
+constexpr int64_t kXChunk = 128;
+__host__ __device__ inline int64_t x_chunks(int64_t max_nx) { return (max_nx + kXChunk - 1) / kXChunk; }
+__host__ __device__ inline int64_t off_xflag(int P, int64_t max_nx) {
   return off_stage(P) + int64_t(2) * 2 * 2 * max_nx * 8;
+}
+__host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
+  return off_xflag(P, max_nx) + int64_t(2) * 2 * x_chunks(max_nx) * 8;
 }
 
 struct PeerArgs {
@@ -47,25 +54,40 @@ __device__ __forceinline__ double* red_slot(char* b, int P, int par, int q) {
 }
 // staging rows: side 0 = "lo" (the previous rank's last two rows), 1 = "hi" (the next rank's
 // first two rows)
-__device__ __forceinline__ double* stage(char* b, int P, int64_t max_nx, int par, int side,
+__host__ __device__ inline double* stage(char* b, int P, int64_t max_nx, int par, int side,
                                          int row) {
   return reinterpret_cast<double*>(b + off_stage(P)) + ((int64_t(par) * 2 + side) * 2 + row) * max_nx;
 }
 
+__device__ __forceinline__ uint64_t* xflag(char* b, int P, int64_t max_nx, int par, int side,
+                                           int64_t ch) {
+  return reinterpret_cast<uint64_t*>(b + off_xflag(P, max_nx)) + (par * 2 + side) * x_chunks(max_nx) + ch;
+}
+
 constexpr uint64_t kSpinMax = uint64_t(1) << 27;  // polls of ~150 ns: ~20 s
 
-// Wait (one lane) until *flag == tag; false on abort or timeout (error word set).
-__device__ inline bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
-  const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(a.base[a.rank] + kOffAbort);
+// Wait (one lane) until *flag == tag; false on abort (the abort word of my buffer `me`) or
+// timeout, with the error word set.  The polls are relaxed (they read past the caches, system
+// scope) and ONE acquire follows the tag: an acquire per poll would invalidate this XCD's L2 over
+// and over, under the feet of every other block on it (the fused kernel's edge bands wait while
+// the interior bands stream).
+__device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const char* me, int* err) {
+  const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(me + kOffAbort);
   for (uint64_t n = 0;; ++n) {
-    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.tag) return true;
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope
+      return true;
+    }
     if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
         n > kSpinMax) {
-      __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
     __builtin_amdgcn_s_sleep(4);
   }
+}
+__device__ inline bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
+  return wait_flag_tag(flag, a.tag, a.base[a.rank], a.err);
 }
 
 // The second half of a halo exchange, called by every block of the grid after the block wrote

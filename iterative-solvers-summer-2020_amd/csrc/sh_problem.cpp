@@ -341,6 +341,23 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   const double eb = 8.0 * 4 * nx_ * (z ? 2 : nv + 2);
   int rc = NK_OK;
   PeerArgs pa;
+  edge_launched_ = true;
+  if (!split && slab_x_enabled(E_.comm) && E_.comm->take_halo(&pa, nx_)) {
+    // peer-memory communicator: the fused kernel's edge bands exchange the edge rows themselves
+    // (arnoldi.hip "Slab exchange"); the halo rows are read from this rank's staging rows
+    const int par = int(pa.tag & 1);
+    A.x.me = pa.base[pa.rank];
+    A.x.prev = pa.base[(pa.rank - 1 + pa.P) % pa.P];
+    A.x.next = pa.base[(pa.rank + 1) % pa.P];
+    A.x.P = pa.P;
+    A.x.max_nx = pa.max_nx;
+    A.x.tag = pa.tag;
+    A.x.err = pa.err;
+    A.yh = stage(A.x.me, pa.P, pa.max_nx, par, 0, 0);
+    A.yh_ld = pa.max_nx;
+    edge_launched_ = false;
+    return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+  }
   if (!split && peer_fuse_enabled() && E_.comm->take_halo(&pa, nx_)) {
     // peer-memory communicator: the edge rows go straight into the neighbours' staging rows
     // and come back into yh_ in the same launch (no y4_ round trip, no separate halo kernel)
@@ -374,7 +391,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
 
 void SHProblem::void_fused_steps(int count) {
   E_.void_last(K_ARNOLDI, count);
-  if (dist()) E_.void_last(K_ARN_EDGE, count);  // the halo exchange still moves its rows
+  if (dist() && edge_launched_) E_.void_last(K_ARN_EDGE, count);
   if (last_split_) E_.void_last(K_ARN_SLAB, count);
 }
 

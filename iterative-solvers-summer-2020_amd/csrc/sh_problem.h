@@ -59,6 +59,7 @@ class SHProblem final : public Problem {
   int64_t mb_cap_ = 0;
   uint64_t mb_tag_ = 0;   // one tag per fused launch
   bool last_split_ = false;  // the last fused step ran as interior + edge-band launches
+  bool edge_launched_ = false;  // the last fused step launched the slab edge kernel
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):

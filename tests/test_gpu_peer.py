@@ -35,7 +35,11 @@ def _single(N, U0, **kw):
     return ref
 
 
-def test_peer_world1_matches_single_slab():
+@pytest.mark.parametrize("xk", ["0", "2"])
+def test_peer_world1_matches_single_slab(xk, monkeypatch):
+    """A world of one through the peer communicator: the edge + halo kernel (xk 0) and the fused
+    kernel's in-kernel slab exchange (NKHIP_SLAB_XK=2; the rank is its own neighbour)."""
+    monkeypatch.setenv("NKHIP_SLAB_XK", xk)
     import nkhip
     N = 96
     U0 = np.random.default_rng(2020).standard_normal((N, N))
@@ -127,13 +131,18 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,N,steps", [(2, 128, 2), (2, 61, 1), (3, 96, 1), (4, 128, 1),
-                                          (8, 256, 1)])
-def test_peer_processes_match_single_slab(world, N, steps, tmp_path):
+@pytest.mark.parametrize("world,N,steps,xk", [(2, 128, 2, "auto"), (2, 61, 1, "auto"),
+                                             (3, 96, 1, "auto"), (4, 128, 1, "auto"),
+                                             (8, 256, 1, "auto"), (2, 128, 2, "1"),
+                                             (3, 96, 1, "1"), (4, 256, 1, "1")])
+def test_peer_processes_match_single_slab(world, N, steps, xk, tmp_path):
     """``world`` processes on one GPU, one slab each, the peer buffers mapped through IPC
     (dmabuf) handles: the gathered slabs equal the single-slab steps.  World 2 has prev == next
     (both halo directions go to one peer); N = 61 takes the point kernel (odd nx); 8 x 256 runs
-    the fused Arnoldi step on 32-row slabs with the device-side control."""
+    the fused Arnoldi step on 32-row slabs with the device-side control.  xk = "1": the fused
+    kernel's edge bands run the slab exchange themselves (NKHIP_SLAB_XK=1 forces it although the
+    ranks share this GPU: the ranks' grids then wait on each other's edge bands, which always
+    progresses -- publishing never waits -- but slowly; "auto" takes the edge + halo kernel)."""
     import subprocess
     U0 = np.random.default_rng(2020).standard_normal((N, N))
     import nkhip
@@ -151,6 +160,8 @@ def test_peer_processes_match_single_slab(world, N, steps, tmp_path):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), GRID_N=str(N), GRID_STEPS=str(steps),
                    OUT_DIR=str(tmp_path), LOCAL_RANK="0")
+        if xk != "auto":
+            env["NKHIP_SLAB_XK"] = xk
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
