@@ -58,7 +58,11 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              const double* y, double alpha, const double* uval, const double* F,
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s,
-                             const double* znorm2 = nullptr, double omega = 0.0);
+                             const double* znorm2 = nullptr, double omega = 0.0,
+                             const double* prm = nullptr);
+// prm (both residual launches; device-side Arnoldi control, nk_kernels.h kCtlPrm): alpha and
+// the FD step sc from the control's parameter block (entries kArnMaxNV + 1, + 2); a step the
+// control handed back (entry kArnMaxNV + 3) does nothing.
 
 // compute_U2 (:413-423): u = eps + sum_d (1-eps) H2(G2(|x - x_d|, R_d), R_d, V_d) at the node
 // coordinates x = (M.dksi, M.deta); `drops` holds ndrops (x, y, R, V) quadruples (by value).
@@ -90,7 +94,8 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
                              const double* x, const double* y, double alpha, const double* uval,
                              const double* cn, int mode, const double* f0, double sc, double* out,
                              double* xt, double* uxx, double* uyy, double* partial, hipStream_t s,
-                             const double* znorm2 = nullptr, double omega = 0.0);
+                             const double* znorm2 = nullptr, double omega = 0.0,
+                             const double* prm = nullptr);
 
 // Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
 // Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the four DCT operands of the MFMA path in

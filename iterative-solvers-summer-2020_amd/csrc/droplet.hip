@@ -13,6 +13,7 @@
 
 #include "droplet.h"
 #include "nk_device.h"
+#include "nk_kernels.h"
 
 namespace nk {
 namespace {
@@ -414,8 +415,13 @@ __global__ void __launch_bounds__(DB) drop_resid_kernel(DropParams P, Coefs Ck, 
                                                         double dt, int mode, const double* f0,
                                                         double sc, double* out, double* xt,
                                                         double* partial, const double* znorm2,
-                                                        double omega) {
+                                                        double omega, const double* prm) {
   const Coefs& C = Ck;
+  if (prm) {  // device-side Arnoldi control: the step's parameters (a handed-back step: nothing)
+    if (prm[kArnMaxNV + 3] != 0.0) return;
+    alpha = prm[kArnMaxNV + 1];
+    sc = prm[kArnMaxNV + 2];
+  }
   if (znorm2) {  // the FD step from the device value |z|^2 (KrylovJacobian.matvec, _nonlin.py:
                  // 1505-1509, with v = z/|z|): the host's sc = omega/|v|, alpha = sc/|z|
     const double hn = sqrt(*znorm2);
@@ -508,8 +514,14 @@ __global__ void __launch_bounds__(DB) mems_resid_kernel(DropParams P, Coefs Ck, 
                                                         int mode, const double* f0, double sc,
                                                         double* out, double* xt, double* uxx,
                                                         double* uyy, double* partial,
-                                                        const double* znorm2, double omega) {
+                                                        const double* znorm2, double omega,
+                                                        const double* prm) {
   const Coefs& C = Ck;
+  if (prm) {  // device-side Arnoldi control (as drop_resid_kernel)
+    if (prm[kArnMaxNV + 3] != 0.0) return;
+    alpha = prm[kArnMaxNV + 1];
+    sc = prm[kArnMaxNV + 2];
+  }
   if (znorm2) {  // the FD step from the device value |y|^2 (as drop_resid_kernel)
     const double hn = sqrt(*znorm2);
     double sig = 1.0 / hn;
@@ -934,7 +946,7 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              const double* y, double alpha, const double* uval, const double* F,
                              double dt, int mode, const double* f0, double sc, double* out,
                              double* xt, double* partial, hipStream_t s, const double* znorm2,
-                             double omega) {
+                             double omega, const double* prm) {
   if (!shape_ok(P)) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
   static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
@@ -944,10 +956,10 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(drop_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S,
-                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega);
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega, prm);
   } else {
     hipLaunchKernelGGL(drop_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S,
-                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega);
+                       x, y, alpha, uval, F, dt, mode, f0, sc, out, xt, partial, znorm2, omega, prm);
   }
   return hipGetLastError();
 }
@@ -964,7 +976,7 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
                              const double* x, const double* y, double alpha, const double* uval,
                              const double* cn, int mode, const double* f0, double sc, double* out,
                              double* xt, double* uxx, double* uyy, double* partial, hipStream_t s,
-                             const double* znorm2, double omega) {
+                             const double* znorm2, double omega, const double* prm) {
   if (!shape_ok(P) || mode < 0 || mode > 2) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
   static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
@@ -975,11 +987,11 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(mems_resid_kernel<true>, dim3(1), dim3(DB), lds, s, P, make_coefs(P), Mp,
                        M, S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial, znorm2,
-                       omega);
+                       omega, prm);
   } else {
     hipLaunchKernelGGL(mems_resid_kernel<false>, dim3(1), dim3(DB), 0, s, P, make_coefs(P), Mp, M,
                        S, x, y, alpha, uval, cn, mode, f0, sc, out, xt, uxx, uyy, partial, znorm2,
-                       omega);
+                       omega, prm);
   }
   return hipGetLastError();
 }

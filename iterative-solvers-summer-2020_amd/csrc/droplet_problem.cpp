@@ -90,6 +90,14 @@ int DropletProblem::jvp_dev(const double* x0, const double* G0, const double* z,
   });
 }
 
+int DropletProblem::jvp_prm(const double* x0, const double* G0, const double* z,
+                            const double* prm, double* w) {
+  return E_.launch(K_USERF, 0.0, [&] {
+    return drop_resid_launch(P_, M_, S_, x0, z, 0.0, uval, F, dt_, 1, G0, 1.0, w, nullptr, nullptr,
+                             E_.s, nullptr, 0.0, prm);
+  });
+}
+
 // ============================================================================================
 // DropletStepper
 // ============================================================================================

@@ -26,6 +26,12 @@ class DropletProblem : public Problem {
   bool has_dev_scale() const override { return true; }
   int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
               double omega, double* w) override;
+  // the LGMRES inner loop under device-side control (no host round trip per Arnoldi step): each
+  // step is a 5551-point single-workgroup residual plus small Krylov launches, latency-bound
+  bool has_jvp_prm() const override { return true; }
+  int jvp_prm(const double* x0, const double* G0, const double* z, const double* prm,
+              double* w) override;
+  bool prefers_devctl() const override { return true; }
   const DropMesh& mesh() const { return M_; }
   const DropScratch& scratch() const { return S_; }
   const DropParams& params() const { return P_; }

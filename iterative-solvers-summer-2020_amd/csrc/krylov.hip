@@ -144,7 +144,13 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
 template <bool VEC, bool NT, int UNR>
 __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
                                                    VecList P, int np, int64_t n, int cpb,
-                                                   double* partial, bool rev) {
+                                                   double* partial, bool rev, const double* prm) {
+  // prm (device-side Arnoldi control): cin and the coefficients from the control's parameter
+  // block; a step the control handed back does nothing
+  if (prm) {
+    if (prm[kArnMaxNV + 3] != 0.0) return;
+    cin = prm[kArnMaxNV];
+  }
   const int64_t nblk = gridDim.x;
   const int64_t bid = blockIdx.x;
   double red[2] = {0.0, 0.0};
@@ -173,7 +179,7 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const double c = P.c[i + u];
+        const double c = prm ? prm[i + u] : P.c[i + u];
 #pragma unroll
         for (int k = 0; k < PAIRS; ++k) {
           acc[k].x += c * pv[u][k].x;
@@ -183,7 +189,7 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
     }
     for (; i < np; ++i) {
       const double* p = P.p[i];
-      const double c = P.c[i];
+      const double c = prm ? prm[i] : P.c[i];
       double2 pv[PAIRS];
 #pragma unroll
       for (int k = 0; k < PAIRS; ++k) pv[k] = ld2s<VEC, NT>(p, base + k * 2 * BS, n);
@@ -335,8 +341,9 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
   return hipGetLastError();
 }
 
-hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
-                        int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
+namespace {
+hipError_t combo_any(double* out, const double* in, double cin, const VecList& P, int np,
+                     int64_t n, double* partial, hipStream_t s, int64_t* nblk, const double* prm) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
   static const int target = env_int("NKHIP_COMBO_BLOCKS", 1 << 30);
   int cpb = 0;
@@ -351,21 +358,33 @@ hipError_t combo_launch(double* out, const double* in, double cin, const VecList
   if (nb <= kSmallChunks) {  // small vectors: 8 basis vectors' loads in flight per batch
     if (vec)
       hipLaunchKernelGGL((combo_kernel<true, false, 8>), grid, block, 0, s, out, in, cin, P, np, n,
-                         cpb, partial, rev);
+                         cpb, partial, rev, prm);
     else
       hipLaunchKernelGGL((combo_kernel<false, false, 8>), grid, block, 0, s, out, in, cin, P, np,
-                         n, cpb, partial, rev);
+                         n, cpb, partial, rev, prm);
   } else if (vec && nt) {
     hipLaunchKernelGGL((combo_kernel<true, true, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev);
+                       cpb, partial, rev, prm);
   } else if (vec) {
     hipLaunchKernelGGL((combo_kernel<true, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev);
+                       cpb, partial, rev, prm);
   } else {
     hipLaunchKernelGGL((combo_kernel<false, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev);
+                       cpb, partial, rev, prm);
   }
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
+                        int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
+  return combo_any(out, in, cin, P, np, n, partial, s, nblk, nullptr);
+}
+
+hipError_t combo_prm_launch(double* out, const double* in, const double* prm, const VecList& P,
+                            int np, int64_t n, hipStream_t s) {
+  if (!prm || np > kArnMaxNV) return hipErrorInvalidValue;
+  return combo_any(out, in, 0.0, P, np, n, nullptr, s, nullptr, prm);
 }
 
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,

@@ -108,7 +108,7 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   const int64_t n = E_.n;
   const int K = int(outer_.size());
   const bool lag = lag_enabled() && P_.may_speculate();
-  const bool devctl = lag && devctl_enabled(E_.comm != nullptr);
+  const bool devctl = lag && devctl_enabled(E_.comm != nullptr || P_.prefers_devctl());
   V_[0] = Fx_;  // v0 = b / |b|, kept raw with scale 1/|b|
   // the loop state (shared with the device-side control: nk_kernels.h ArnCtlState)
   ArnCtlState& S = *hS_;
@@ -291,10 +291,22 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
         sig_est[j + 1] = 0.0;
       }
       rc = issue_step(j + 1, z, zs, zn, false);
-      if (!rc) rc = E_.sync();
       if (rc) return rc;
       hn_pending = true;
       ++j;
+      if (devctl && next_is_v && P_.has_jvp_prm() && zn != 0.0) {
+        // the following steps under device-side control, unfused (update, JVP, multi-dot and
+        // the reduction + control per step, no host round trip)
+        S.j = j;
+        S.hn_pending = 1;
+        rc = device_steps();
+        j = S.j;
+        hn_pending = S.hn_pending != 0;
+        if (rc) return rc;
+        continue;
+      }
+      rc = E_.sync();
+      if (rc) return rc;
       continue;
     }
     // -- v_{j+1} = tau w - V h and its exact |v_{j+1}|^2 before the next JVP
@@ -379,7 +391,9 @@ int NewtonKrylov::device_steps() {
   const int t0 = S.j;
   // the largest basis length the device issues fused steps for (every length up to it runs fused)
   int nvmax = t0;
-  while (nvmax + 1 < S.m && nvmax + 1 <= kArnMaxNV && P_.has_fused(nvmax + 1)) ++nvmax;
+  while (nvmax + 1 < S.m && nvmax + 1 <= kArnMaxNV &&
+         (P_.has_fused(nvmax + 1) || P_.has_jvp_prm()))
+    ++nvmax;
   if (nvmax < t0 + 1) return E_.wait_results(Engine::slot_mdot(t0), 2 * (t0 + 1) + 1);
   S.nv_max = nvmax;
   S.halt = 0;
@@ -401,6 +415,7 @@ int NewtonKrylov::device_steps() {
     double* spare;
     double* v;
     bool fused;
+    bool unfused;  // an unfused device step (update in place, JVP, multi-dot): nothing to rotate
   };
   Rot rot[kMaxVec + 2];
   double cc[kMaxVec] = {};  // the launch arguments the parameter block overrides
@@ -417,7 +432,38 @@ int NewtonKrylov::device_steps() {
   // the fused step nv = t + 1 with the parameters control t writes, its reduction into the slot
   // of step t + 1 and the control of step t + 1
   auto issue = [&](int t) -> int {
-    rot[t] = Rot{Sv_, V_[t + 1], false};
+    rot[t] = Rot{Sv_, V_[t + 1], false, false};
+    const int nval = 2 * (t + 2) + 1;
+    const int slot = Engine::slot_mdot(t + 1);
+    if (!P_.has_fused(t + 1)) {
+      // unfused: v_{t+1} = tau w + sum c_i V_i in place of w = V_[t+1] (coefficients from the
+      // parameter block), w' = J v_{t+1} -> V_[t+2], then the multi-dot of w' and v_{t+1}
+      // against V_0..V_{t+1} -- the fused kernel's result layout, so the same reduction + control
+      const int64_t n = E_.n;
+      double* w = V_[t + 1];
+      VecList U;
+      for (int i = 0; i <= t; ++i) U.p[i] = V_[i];
+      int rc = E_.launch(K_COMBO, 8.0 * n * (t + 3),
+                         [&] { return combo_prm_launch(w, w, prm_, U, t + 1, n, E_.s); });
+      if (!rc) rc = P_.jvp_prm(X_, G0_, w, prm_, V_[t + 2]);
+      if (rc) return rc;
+      zp_[t + 1] = w;
+      rot[t].unfused = true;
+      VecList Pm;
+      for (int i = 0; i <= t + 1; ++i) Pm.p[i] = V_[i];
+      int64_t nb = 0;
+      rc = E_.launch(K_MDOT, 8.0 * n * (t + 4), [&] {
+        return mdot_launch(V_[t + 2], w, Pm, t + 2, n, E_.partial(), E_.s, &nb);
+      });
+      if (rc) return rc;
+      if (one)
+        return E_.launch(K_CTL, 8.0 * nb * nval, [&] {
+          return arn_reduce_ctl_launch(E_.partial(), nb, nval, E_.dres_mut(slot),
+                                       E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
+        });
+      rc = E_.reduce_async(nb, nval, nval, slot, false);
+      return rc ? rc : control(t + 1, true);
+    }
     const double* Vp[kMaxVec];
     for (int i = 0; i <= t; ++i) Vp[i] = V_[i];
     double* vout = Sv_;
@@ -429,8 +475,6 @@ int NewtonKrylov::device_steps() {
     V_[t + 1] = vout;
     zp_[t + 1] = vout;
     rot[t].fused = true;
-    const int nval = 2 * (t + 2) + 1;
-    const int slot = Engine::slot_mdot(t + 1);
     if (one)
       return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
         return arn_reduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
@@ -465,8 +509,12 @@ int NewtonKrylov::device_steps() {
     if (next == t && next + 1 <= nvmax) rc = issue(next++);
   }
   // step t was handed back: the fused steps queued from t on do nothing; undo their rotations
-  int voided = 0;
+  int voided = 0, voided_unfused = 0;
   for (int u = next - 1; u >= t; --u) {
+    if (rot[u].unfused) {  // its update and JVP saw the halt: V_[u+1], V_[u+2] untouched
+      ++voided_unfused;
+      continue;
+    }
     if (!rot[u].fused) continue;
     Sv_ = rot[u].spare;
     V_[u + 1] = rot[u].v;
@@ -475,7 +523,10 @@ int NewtonKrylov::device_steps() {
   // ... and their launches did no work: out of the kernel profile (the fused launches, and the
   // reduction + control launches each of those steps queued behind it)
   P_.void_fused_steps(voided);
-  E_.void_last(K_CTL, voided);
+  E_.void_last(K_CTL, voided + voided_unfused);
+  E_.void_last(K_COMBO, voided_unfused);
+  E_.void_last(K_USERF, voided_unfused);
+  E_.void_last(K_MDOT, voided_unfused);
   if (!one) E_.void_last(K_REDUCE, voided);
   if (rc) return rc;
   // The voided reduction of slot_mdot(t + 1) may still write that pinned host slot after the

@@ -48,6 +48,14 @@ int MemsProblem::jvp_dev(const double* x0, const double* G0, const double* z,
   });
 }
 
+int MemsProblem::jvp_prm(const double* x0, const double* G0, const double* z, const double* prm,
+                         double* w) {
+  return E_.launch(K_USERF, 0.0, [&] {
+    return mems_resid_launch(P_, Mp_, M_, S_, x0, z, 0.0, uval, F, 1, G0, 1.0, w, nullptr, nullptr,
+                             nullptr, nullptr, E_.s, nullptr, 0.0, prm);
+  });
+}
+
 MemsStepper::MemsStepper(const DropParams& Pp, const MemsParams& Mp, double epsilon,
                          const nk_opts& o, hipStream_t s)
     : opts(o), E(int64_t(Pp.nx) * Pp.ny, nullptr, s, o.profile != 0, 16), P(E, Pp, Mp),

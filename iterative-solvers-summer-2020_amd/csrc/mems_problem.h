@@ -21,6 +21,8 @@ class MemsProblem final : public DropletProblem {
           double* w) override;
   int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
               double omega, double* w) override;
+  int jvp_prm(const double* x0, const double* G0, const double* z, const double* prm,
+              double* w) override;
 
  private:
   MemsParams Mp_;

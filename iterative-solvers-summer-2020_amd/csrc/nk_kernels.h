@@ -108,6 +108,10 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
 // out may alias `in` or any p_i (element-wise, each element read and written by one thread).
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
                         int64_t n, double* partial, hipStream_t s, int64_t* nblk);
+// The same under device-side Arnoldi control: out = prm[kArnMaxNV] in + sum_i prm[i] p_i (the
+// coefficients the control kernel wrote); nothing when the step was handed back (prm halt entry).
+hipError_t combo_prm_launch(double* out, const double* in, const double* prm, const VecList& P,
+                            int np, int64_t n, hipStream_t s);
 // result[k] = sum_b partial[k*nblk + b] for k < nsum, NaN-propagating max for nsum <= k < nv.
 // result_host (optional): pinned host memory the kernel also writes (zero-copy readback).
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,

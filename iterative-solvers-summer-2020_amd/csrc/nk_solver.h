@@ -223,6 +223,16 @@ struct Problem {
   // May the solver evaluate a JVP it later discards (the step after the last Arnoldi step)?  A
   // user callback must see exactly scipy's F calls, so the generic problem says no.
   virtual bool may_speculate() const { return true; }
+  // Device-side Arnoldi control without a fused kernel (lgmres.cpp device_steps): w = J z with
+  // the JVP's scale and FD step from the control's parameter block prm (nk_kernels.h kCtlPrm);
+  // nothing when the step was handed back.  Problems whose Arnoldi steps are latency-bound
+  // launches (the moving-mesh residuals) prefer the device control even on one GPU.
+  virtual bool has_jvp_prm() const { return false; }
+  virtual int jvp_prm(const double* /*x0*/, const double* /*G0*/, const double* /*z*/,
+                      const double* /*prm*/, double* /*w*/) {
+    return NK_EINVAL;
+  }
+  virtual bool prefers_devctl() const { return false; }
   // Fused Arnoldi step (arnoldi.hip): v = tau w + sum c_i V_i -> out_v, w' = J z -> out_w with
   // z = v (z == nullptr) or z = the given vector (scale zs, norm-free step sc), and the multi-dot
   // partials of w' and v against V_0..V_{nv-1}, v; *nwaves = partial columns.
