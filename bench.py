@@ -286,6 +286,41 @@ def config_shlin(sizes=((64, 30, 30), (512, 20, 2))):
     return {"workload": "sh_linearised_semi_implicit_step", **out}
 
 
+def config5_one_gpu(n=16384, warmup=1, steps=1):
+    """Config 5's grid (16384^2, d = 0.625 N, the same parameters and seed) on ONE GPU: the
+    single-GPU point of the 1/2/4/8 strong-scaling series the driver's 8-GPU job measures (the
+    workspace pool is 58 vectors of 2.1 GB = 125 GB of HBM).  steps/s and ms per Arnoldi step."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    U0 = np.random.default_rng(2020).standard_normal((n, n))
+    U = torch.as_tensor(U0, device="cuda")
+    del U0
+    m = nkhip.SwiftHohenberg(N=n, d=0.625 * n, k=0.2, r=0.01, g=1.0)
+    out = torch.empty_like(U)
+    for _ in range(warmup):
+        m.step(U, out=out)
+        U, out = out, U
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    narn = nit = 0
+    for _ in range(steps):
+        m.step(U, out=out)
+        narn += m.last_stats["n_arnoldi"]
+        nit += m.last_stats["nit"]
+        U, out = out, U
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m.close()
+    del U, out
+    torch.cuda.empty_cache()
+    return {"workload": f"swift_hohenberg_cn_newton_krylov_{n}x{n}_1gpu", "steps": steps,
+            "warmup": warmup, "gpu_steps_per_s": round(steps / dt, 4),
+            "ms_per_arnoldi_step": round(1e3 * dt / max(narn, 1), 3),
+            "newton_its_per_step": nit / steps, "arnoldi_steps_per_step": narn / steps}
+
+
 def config_droplet_init():
     """initialise_coalescing_droplets(1000, [[0,0,1,1],[3,0,1,1]], 5e-9, 20) on
     the GPU (20 000 PMA loops); checked against the reference's initdrop_coal_* file."""
@@ -603,6 +638,7 @@ def main():
             out["cpu_baseline"] = rec
         if world == 1 and args.extra == "on":
             out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet(),
+                                    "config5_1gpu": config5_one_gpu(),
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),
                                     "droplet_init": config_droplet_init()}
         print(json.dumps(out), flush=True)
