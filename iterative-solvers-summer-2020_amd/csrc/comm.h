@@ -34,6 +34,8 @@ struct nk_comm {
   // the ranks' kernels share one device (loopback): launches of different ranks run
   // concurrently, so a kernel cannot count on its whole grid being resident
   virtual bool shares_device() const { return false; }
+  // some two ranks of the group share a device (the same answer on every rank)
+  virtual bool group_shares_device() const { return shares_device(); }
   // a collective already enqueued on the device failed (peer-memory communicator: a wait timed
   // out or the group was aborted); checked after each stream synchronisation (Engine::sync)
   virtual bool failed() const { return false; }

@@ -20,7 +20,7 @@ struct PeerArgs;  // peer_dev.h (the peer-memory communicator's device-side argu
 // call) keeps the separate communicator launches.
 bool peer_fuse_enabled();
 // The fused kernel runs the slab exchange itself (arnoldi.hip "Slab exchange"), with the peer
-// communicator (and NKHIP_PEER_FUSE on): NKHIP_SLAB_XK=2 when the ranks do not share a GPU, 1
+// communicator (and NKHIP_PEER_FUSE on): NKHIP_SLAB_XK=2 when no two ranks share a GPU, 1
 // always (tests: several processes on one GPU); unset / 0: off (read per call).
 bool slab_x_enabled(const nk_comm* c);
 

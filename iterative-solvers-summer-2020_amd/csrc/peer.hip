@@ -109,7 +109,7 @@ struct PeerComm final : nk_comm {
   int* err = nullptr;  // pinned host
   hipStream_t side = nullptr;  // abort writes (never queued behind a spinning collective)
   uint64_t red_tag = 0, halo_tag = 0;
-  bool connected = false, same_dev = false, aborted = false;
+  bool connected = false, same_dev = false, any_shared = false, aborted = false;
   PeerBlob blob{};
 
   ~PeerComm() override {
@@ -123,6 +123,7 @@ struct PeerComm final : nk_comm {
   int rank() const override { return r; }
   int size() const override { return p; }
   bool shares_device() const override { return same_dev; }
+  bool group_shares_device() const override { return any_shared; }
   bool failed() const override {
     return aborted || (err && __atomic_load_n(err, __ATOMIC_ACQUIRE) != 0);
   }
@@ -205,7 +206,7 @@ bool peer_fuse_enabled() {
 bool slab_x_enabled(const nk_comm* c) {
   const char* e = std::getenv("NKHIP_SLAB_XK");
   if (!(e && (e[0] == '1' || e[0] == '2')) || !c || !peer_fuse_enabled()) return false;
-  return e[0] == '1' || !c->shares_device();
+  return e[0] == '1' || !c->group_shares_device();
 }
 
 int comm_peer_handle_bytes() { return int(sizeof(PeerBlob)); }
@@ -259,6 +260,11 @@ int comm_peer_connect(nk_comm* comm, const void* handles) {
   if (std::memcmp(&blobs[c->r], &c->blob, sizeof(PeerBlob)) != 0) return NK_EINVAL;
   c->base.assign(c->p, nullptr);
   c->opened.assign(c->p, false);
+  for (int q1 = 0; q1 < c->p; ++q1)  // every rank sees every blob: the same answer everywhere
+    for (int q2 = q1 + 1; q2 < c->p; ++q2)
+      if (blobs[q1].bus == blobs[q2].bus && blobs[q1].dev == blobs[q2].dev &&
+          blobs[q1].domain == blobs[q2].domain)
+        c->any_shared = true;
   for (int q = 0; q < c->p; ++q) {
     const PeerBlob& b = blobs[q];
     if (b.bytes != c->bytes) return NK_EINVAL;  // every rank built for the same group shape
