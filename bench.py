@@ -56,6 +56,9 @@ def parse():
                          "WRITE_SIZE) over a short child run of this bench, N=1 only")
     ap.add_argument("--probes", choices=["on", "off"], default="on",
                     help="the isolated-JVP and copy-bandwidth probes after the timed region")
+    ap.add_argument("--slab-ab", type=int, default=2,
+                    help="N > 1: time steps of each slab-exchange variant after the timed region "
+                         "(slab_exchange_ab; 0: off)")
     return ap.parse_args()
 
 
@@ -413,26 +416,29 @@ def copy_bandwidth(n, reps=20):
                     "after the timed region"}
 
 
-def peer_or_rccl(nkhip, dist, torch, max_nx):
+def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cuda", allow_rccl=True):
     """The peer-memory communicator, verified before it is used: one all-reduce and one halo
-    exchange of known values through it (nk_comm_selftest; device waits are bounded).  If any
-    rank cannot create, map or verify it, every rank falls back to RCCL (stderr says so)."""
+    exchange of known values through it, at the full row width (nk_comm_selftest; device waits
+    are bounded).  If any rank cannot create, map or verify it, every rank falls back to RCCL
+    (stderr says so) -- or fails, when the ranks share a device (RCCL takes one rank per GPU)."""
     comm, ok = None, 1
     try:
         comm = nkhip.PeerComm.from_torch_distributed(max_nx=max_nx)
-        ok = int(comm.selftest(min(max_nx, 4096)))
+        ok = int(comm.selftest(max_nx))
     except Exception as e:  # noqa: BLE001 - any failure means: use RCCL instead
         print(f"peer-memory communicator unavailable: {e}", file=sys.stderr)
         ok = 0
-    flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+    flag = torch.tensor([ok], dtype=torch.int32, device=coll_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 1:
         return comm
-    print("peer-memory communicator failed its self-test on some rank: using RCCL",
-          file=sys.stderr)
+    print("peer-memory communicator failed its self-test on some rank"
+          + (": using RCCL" if allow_rccl else ""), file=sys.stderr)
     if comm is not None:
         comm.abort()
         comm.close()
+    if not allow_rccl:
+        raise RuntimeError("peer-memory communicator failed and the ranks share a device")
     return nkhip.RcclComm.from_torch_distributed()
 
 
@@ -445,35 +451,130 @@ def load_traffic():
         return {}
 
 
+def self_launch(n):
+    """``--gpus N`` started without a launcher (no WORLD_SIZE in the environment): start N rank
+    processes of this same command line, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run sets them), forward rank 0's
+    JSON line as this process's only stdout line and return the exit code (non-zero when any rank
+    failed; the survivors are killed 60 s after the first failure, their peer waits being bounded).
+    Runs before this process imports anything that touches the GPU, and it execs nothing: the
+    ranks are children.  NKHIP_BENCH_ONE_DEVICE=1 puts every rank on device 0 (testing on a
+    one-GPU box: the ranks' side channel is then gloo, as RCCL takes one rank per device)."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        # rank 0's stdout carries the JSON line; the other ranks print nothing there
+        procs.append(subprocess.Popen(cmd, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode()
+                                                         .splitlines()), daemon=True)
+    reader.start()
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+            print("bench: a rank failed; stopping the others in 60 s", file=sys.stderr)
+        if failed_at is not None and time.monotonic() - failed_at > 60:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    reader.join(30)
+    rcs = [p.returncode for p in procs]
+    lines = [ln for ln in out0 if ln.startswith("{")]
+    for ln in out0:
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if any(rcs) or len(lines) != 1:
+        print(f"bench: rank exit codes {rcs}, {len(lines)} JSON line(s) from rank 0",
+              file=sys.stderr)
+        return next((c for c in rcs if c), 1)
+    print(lines[0], flush=True)
+    return 0
+
+
+def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
+    """N > 1, after the timed region: the two slab-exchange variants of the fused Arnoldi step,
+    alternating one time step each (``rounds`` of each), as ms per Arnoldi step (max over ranks
+    of each step's wall time ÷ its Arnoldi steps).  edge_halo: the default -- a 4-row edge kernel
+    that exchanges u on the slab's edge rows, then the fused pass; in_kernel: the fused pass's
+    edge bands exchange them themselves (NKHIP_SLAB_XK=2; =1 when the ranks share a GPU), the
+    interior bands never wait.  Returns (record, a, b) with the trajectory advanced."""
+    old = os.environ.get("NKHIP_SLAB_XK")
+    acc = {"edge_halo": [0.0, 0], "in_kernel": [0.0, 0]}
+    try:
+        for i in range(2 * rounds):
+            name = "edge_halo" if i % 2 == 0 else "in_kernel"
+            os.environ["NKHIP_SLAB_XK"] = ("1" if one_device else "2") if i % 2 else "0"
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            model.step(a, out=b)
+            torch.cuda.synchronize()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            acc[name][0] += float(t.item())
+            acc[name][1] += model.last_stats["njvp"]
+            a, b = b, a
+    finally:
+        if old is None:
+            os.environ.pop("NKHIP_SLAB_XK", None)
+        else:
+            os.environ["NKHIP_SLAB_XK"] = old
+    rec = {f"{k_}_ms_per_arnoldi": round(1e3 * v[0] / max(v[1], 1), 4) for k_, v in acc.items()}
+    rec.update({"steps_each": rounds, "arnoldi_steps": {k_: v[1] for k_, v in acc.items()},
+                "what": "alternating time steps after the timed region; max over ranks of each "
+                        "step's wall time / its Arnoldi steps"})
+    return rec, a, b
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))  # before anything touches the GPU
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import nkhip
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
-            sys.exit(2)
-    torch.cuda.set_device(local)
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    # testing on one GPU: every rank on device 0 (gloo side channel, peer communicator only)
+    one_device = world > 1 and os.environ.get("NKHIP_BENCH_ONE_DEVICE") == "1"
+    device = 0 if one_device else local
+    torch.cuda.set_device(device)
     comm = None
     use_dist = world > 1 or args.rccl_self or args.peer_self
+    coll_dev = "cpu" if one_device else "cuda"  # where torch.distributed's tensors live
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1:  # --rccl-self / --peer-self without a launcher: a world of one
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
             os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         if args.rccl_self or (world > 1 and args.comm == "rccl" and not args.peer_self):
             comm = nkhip.RcclComm.from_torch_distributed()
         else:
-            comm = peer_or_rccl(nkhip, dist, torch, args.n)
+            comm = peer_or_rccl(nkhip, dist, torch, args.n, coll_dev, allow_rccl=not one_device)
 
     n = args.n
     h, k, r, g = 0.625, 0.2, 0.01, 1.0
@@ -485,6 +586,10 @@ def main():
     # kernel timing: HIP events around every PROFILE-th launch of each kernel class inside the
     # timed region (an event pair costs ~5 us of GPU time; every launch timed costs ~7 %)
     profile = int(os.environ.get("NKHIP_BENCH_PROFILE", "8"))
+    if use_dist:
+        # the problem's first device collective runs inside its construction: no rank may reach
+        # it seconds ahead of a peer still generating its state (the device waits are bounded)
+        dist.barrier()
     model = nkhip.SwiftHohenberg(N=n, d=h * n, k=k, r=r, g=g, jvp=args.jvp, profile=profile,
                                  comm=comm, ny_local=ny, stream=stream)
     a, b = U, torch.empty_like(U)
@@ -511,24 +616,35 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     prof = model.kernel_profile()
     final_max = float(a.abs().max())
     # check the final step on the host (outside the timed region): a = U[s+1], b = U[s]; with
     # N > 1 the slabs are gathered to every rank and rank 0 evaluates the oracle residual
-    # (sh_scipy_nk.py:47-49) of the whole grid
+    # (sh_scipy_nk.py:47-49) of the whole grid.  Slabs differ in rows by at most one: gathered
+    # padded to the largest slab, then trimmed.
     if world > 1:
-        ga = [torch.empty_like(a) for _ in range(world)]
-        gb = [torch.empty_like(b) for _ in range(world)]
-        dist.all_gather(ga, a.contiguous())
-        dist.all_gather(gb, b.contiguous())
-        full_a = torch.cat(ga).cpu().numpy() if rank == 0 else None
-        full_b = torch.cat(gb).cpu().numpy() if rank == 0 else None
-        del ga, gb
+        nys = [nkhip.slab_rows(n, q, world)[1] for q in range(world)]
+        nymax = max(nys)
+
+        def gather(x):
+            xp = torch.zeros((nymax, n), dtype=x.dtype, device=coll_dev)
+            xp[:ny] = x.to(coll_dev)
+            parts = [torch.empty_like(xp) for _ in range(world)]
+            dist.all_gather(parts, xp)
+            if rank != 0:
+                return None
+            return torch.cat([p_[:nq] for p_, nq in zip(parts, nys)]).cpu().numpy()
+
+        full_a, full_b = gather(a), gather(b)
     else:
         full_a, full_b = a.cpu().numpy(), b.cpu().numpy()
+    slab_ab = None
+    if world > 1 and args.slab_ab > 0:
+        slab_ab, a, b = slab_exchange_ab(model, a, b, args.slab_ab, one_device, dist, coll_dev,
+                                         torch)
 
     if rank == 0:
         steps_per_s = args.steps / elapsed
@@ -536,7 +652,12 @@ def main():
         ker = {k_: v for k_, v in prof.items() if v["timed"] > 0 and v["ms"] > 0}
         for v in ker.values():  # whole-class time extrapolated from the timed launches
             v["ms_est"] = v["ms"] * v["launches"] / v["timed"]
-        dom = max(ker, key=lambda k_: ker[k_]["ms_est"]) if ker else None
+        # the dominant HBM-streaming class; the slab path's exchange / control launches are
+        # latency-bound (their time is waiting for peers, not bytes) and are reported in
+        # "kernels" beside it
+        comm_classes = {"arnoldi_edge", "halo", "arnoldi_ctl", "reduce_final", "edge_gather"}
+        cand = [k_ for k_ in ker if k_ not in comm_classes] or list(ker)
+        dom = max(cand, key=lambda k_: ker[k_]["ms_est"]) if cand else None
 
         # PMC traffic of this run (two child passes under rocprofv3), else the last profile's
         live = pmc_traffic(args) if (world == 1 and args.pmc == "auto") else None
@@ -605,6 +726,10 @@ def main():
             "final_step_check": final_check,
             "cpu_baseline": None,
         }
+        if slab_ab is not None:
+            out["slab_exchange_ab"] = slab_ab
+        if one_device:
+            out["config"]["ranks_on_one_device"] = True
         out["traffic_measurement"] = (
             {"live": True, "seconds": live.get("seconds"),
              "classes": {c: round(v["traffic_over_alg"], 4) for c, v in live["classes"].items()

@@ -192,12 +192,15 @@ int nk_comm_create_rccl(nk_comm** out, const void* unique_id, int32_t rank, int3
 /* One process, `nranks` slabs driven by `nranks` host threads on one device (testing the slab
  * logic on a single GPU): fills out[0..nranks-1]. */
 int nk_comm_create_loopback(nk_comm** out, int32_t nranks);
-/* Peer-memory communicator (one process per GPU over xGMI, or several processes / threads on
- * one GPU): the slab collectives are small kernels that write straight into the peers' exported
- * buffers and wait for tagged flags (csrc/peer.hip) instead of RCCL calls.  Two phases: create
+/* Peer-memory communicator (one process per GPU over xGMI, or several processes on one GPU):
+ * the slab collectives are small kernels that write straight into the peers' exported buffers
+ * and wait for tagged flags (csrc/peer.hip) instead of RCCL calls.  Two phases: create
  * (allocates this rank's buffer for slabs of up to max_nx columns and writes its handle blob,
  * nk_comm_peer_handle_bytes() bytes, to handle_out), exchange the blobs through any side
- * channel, then connect with all nranks blobs in rank order. */
+ * channel, then connect with all nranks blobs in rank order.  One PROCESS per rank: connect
+ * returns NK_EINVAL when two ranks of a group of more than one are the same process (threads
+ * of one process share its in-order hardware queues, so a collective waiting for a peer rank
+ * could sit ahead of the launch it waits for). */
 int nk_comm_peer_handle_bytes(void);
 int nk_comm_create_peer(nk_comm** out, int32_t rank, int32_t nranks, int64_t max_nx,
                         void* handle_out);
@@ -207,7 +210,8 @@ int nk_comm_destroy(nk_comm* c);
  * collective of the group returns NK_ECOMM instead of waiting for the failed rank (the waiting
  * threads are woken).  Peer-memory communicator: the abort word is written into every rank's
  * buffer, so every rank's collective kernels stop waiting and its next synchronisation returns
- * NK_ECOMM (a wait also gives up by itself after ~20 s).  RCCL (one process per GPU): this
+ * NK_ECOMM (a wait also gives up by itself after NKHIP_PEER_TIMEOUT_S seconds of wall-clock
+ * time, default 20).  RCCL (one process per GPU): this
  * rank's communicator is aborted at once (ncclCommAbort) and its later calls return NK_ECOMM;
  * peer processes are NOT notified -- a peer blocked in a collective with the failed rank is
  * released by the launcher's own failure handling (e.g. the torch.distributed watchdog).  A stepper calls it itself when one of its steps fails with a negative code; a host

@@ -291,7 +291,7 @@ __device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0
 // cycle; the interior bands (all but two per column group) never wait at all, which is the
 // overlap: the exchange runs beside the interior of the pass instead of before it (the edge
 // kernel + halo kernel in series, ~22 us per Arnoldi step).  The halo rows are then read from
-// this rank's staging rows (A.yh, row stride A.yh_ld).  A wait that gives up (abort, ~20 s) sets
+// this rank's staging rows (A.yh, row stride A.yh_ld).  A wait that gives up (abort, timeout) sets
 // the communicator's error word; the host sees it at its next synchronisation.
 template <int NV>
 __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW, int h0,
@@ -333,7 +333,8 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
     if (t < nown + 2) {
       const int64_t ch = (t == 0) ? cl : ((t == 1) ? cr : c0 + (t - 2));
       ARN_CHK(ch >= 0 && ch < nch);
-      (void)wait_flag_tag(xflag(X.me, X.P, X.max_nx, par, side, ch), X.tag, X.me, X.err);
+      (void)wait_flag_tag(xflag(X.me, X.P, X.max_nx, par, side, ch), X.tag, X.me, X.err,
+                          X.wait_ticks);
     }
   }
   __syncthreads();
@@ -1412,23 +1413,28 @@ __global__ void __launch_bounds__(256) arnoldi_edge_kernel(const ArnoldiArgs A, 
                                                            int h0, const PeerArgs pa) {
   const double a_tau = arn_tau(A);
   if (arn_halted(A)) return;
-  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (!PEER && j >= A.nx) return;
   const int t = blockIdx.y;
   const int64_t row = (t < 2) ? t : A.ny - 4 + t;
-  const int64_t o = CI(row * A.nx + (j < A.nx ? j : 0), A.ny * A.nx);
-  // the stencil input u of the fused kernel (the kernel is latency-bound: 4 rows of a slab --
-  // every entry load in flight at once; batches of 8 took 10 us per launch)
-  const double y = edge_u<NV>(A, o, h0, a_tau);
   if constexpr (!PEER) {
-    y4[int64_t(t) * A.nx + j] = y;
+    const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (j >= A.nx) return;
+    const int64_t o = CI(row * A.nx + j, A.ny * A.nx);
+    // the stencil input u of the fused kernel (the kernel is latency-bound: 4 rows of a slab --
+    // every entry load in flight at once; batches of 8 took 10 us per launch)
+    y4[int64_t(t) * A.nx + j] = edge_u<NV>(A, o, h0, a_tau);
   } else {
-    // rows 0, 1 are the previous rank's "hi" staging rows, rows ny-2, ny-1 the next rank's "lo"
+    // rows 0, 1 are the previous rank's "hi" staging rows, rows ny-2, ny-1 the next rank's "lo";
+    // a grid of at most kHaloMaxBlocks column blocks strides over wider rows (peer_dev.h: every
+    // block waits in peer_halo_finish, so the grid must fit the GPU as a whole)
     const int par = int(pa.tag & 1);
     const int q = (t < 2) ? (pa.rank - 1 + pa.P) % pa.P : (pa.rank + 1) % pa.P;
-    ARN_CHK(j >= A.nx || j < pa.max_nx);
-    if (j < A.nx) stage(pa.base[q], pa.P, pa.max_nx, par, t < 2 ? 1 : 0, t & 1)[j] = y;
-    (void)peer_halo_finish(pa, j, A.nx, y4, y4 + 2 * A.nx);  // failure: the host finds it
+    double* dst = stage(pa.base[q], pa.P, pa.max_nx, par, t < 2 ? 1 : 0, t & 1);
+    const int64_t step = int64_t(gridDim.x) * 256;
+    for (int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x; j < A.nx; j += step) {
+      ARN_CHK(j < pa.max_nx);
+      dst[j] = edge_u<NV>(A, CI(row * A.nx + j, A.ny * A.nx), h0, a_tau);
+    }
+    (void)peer_halo_finish(pa, A.nx, y4, y4 + 2 * A.nx);  // failure: the host finds it
   }
 }
 
@@ -1441,7 +1447,8 @@ hipError_t edge_launch_nv(const ArnoldiArgs& A, double* y4, int h0, const PeerAr
     if (A.nv != NV) return edge_launch_nv<NV + 1>(A, y4, h0, pa, s);
     const dim3 grid(unsigned((A.nx + 255) / 256), 4);
     if (pa)
-      hipLaunchKernelGGL((arnoldi_edge_kernel<NV, true>), grid, dim3(256), 0, s, A, y4, h0, *pa);
+      hipLaunchKernelGGL((arnoldi_edge_kernel<NV, true>), dim3(unsigned(halo_blocks(A.nx)), 4),
+                         dim3(256), 0, s, A, y4, h0, *pa);
     else
       hipLaunchKernelGGL((arnoldi_edge_kernel<NV, false>), grid, dim3(256), 0, s, A, y4, h0,
                          PeerArgs{});

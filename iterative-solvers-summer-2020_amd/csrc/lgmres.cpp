@@ -499,7 +499,9 @@ int NewtonKrylov::device_steps() {
   while (!rc) {
     const uint32_t v = E_.wait_flag(status_ + t);
     if (v != 1) {
-      if (v != 2) rc = NK_EHIP;  // the control of step t never ran
+      // the control of step t never ran: a collective before it failed (a peer aborted or a
+      // wait timed out: the communicator says so) or a HIP error
+      if (v != 2) rc = (E_.comm && E_.comm->failed()) ? NK_ECOMM : NK_EHIP;
       break;
     }
     st_->njvp += 1;  // step t's fused step is part of the process

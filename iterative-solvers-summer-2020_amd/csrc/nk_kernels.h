@@ -160,6 +160,7 @@ struct SlabX {
   int64_t max_nx = 0;
   uint64_t tag = 0;
   int* err = nullptr;  // pinned host error word of the communicator
+  uint64_t wait_ticks = 0;  // bound of one wait (PeerArgs::wait_ticks)
 };
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;

@@ -24,7 +24,7 @@
 // issue the same collectives in the same order).  Slots and flags are double-buffered by tag
 // parity: a rank can only be one collective ahead of any peer (each collective waits for every
 // peer's contribution to the previous one), so parity t & 1 is never overwritten before it was
-// read.  A wait is bounded: after ~20 s, or once any rank aborted the group (its abort word is
+// read.  A wait is bounded: after NKHIP_PEER_TIMEOUT_S (20 s) of wall-clock time, or once any rank aborted the group (its abort word is
 // written into every peer's buffer), the kernel sets the rank's error word (pinned host memory)
 // and returns; the host turns that into NK_ECOMM (Engine::sync), so peers blocked in a
 // collective with a failed rank return instead of hanging (nkhip.h nk_comm_abort).
@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <random>
 #include <vector>
 
 #include "../../include/nkhip.h"
@@ -79,24 +80,48 @@ __global__ void __launch_bounds__(kHaloBlock) peer_halo_kernel(const PeerArgs a,
                                                                int64_t nx) {
   const int par = int(a.tag & 1);
   const int prev = (a.rank - 1 + a.P) % a.P, next = (a.rank + 1) % a.P;
-  const int64_t c = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x;
-  if (c < nx) {
+  // a grid of at most kHaloMaxBlocks blocks (peer_dev.h: it must fit the GPU as a whole)
+  const int64_t step = int64_t(gridDim.x) * kHaloBlock;
+  for (int64_t c = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x; c < nx; c += step) {
     // my first rows are the previous rank's "hi", my last rows the next rank's "lo"
     stage(a.base[prev], a.P, a.max_nx, par, 1, 0)[c] = v[c];
     stage(a.base[prev], a.P, a.max_nx, par, 1, 1)[c] = v[nx + c];
     stage(a.base[next], a.P, a.max_nx, par, 0, 0)[c] = v[(ny - 2) * nx + c];
     stage(a.base[next], a.P, a.max_nx, par, 0, 1)[c] = v[(ny - 1) * nx + c];
   }
-  peer_halo_finish(a, c, nx, lo, hi);
+  peer_halo_finish(a, nx, lo, hi);
 }
 
 // what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)
 struct PeerBlob {
   hipIpcMemHandle_t ipc;
-  uint64_t ptr;  // the buffer in the owner's address space (used when the peer is the same process)
+  uint64_t ptr;  // the buffer in the owner's address space (used only by the owner itself)
+  uint64_t nonce;  // random per process: with the pid, tells "this process" apart across pid
+                   // namespaces and hosts
   int32_t pid, bus, dev, domain;
   int64_t bytes;
 };
+
+uint64_t process_nonce() {
+  static const uint64_t v = [] {
+    std::random_device rd;
+    uint64_t x = (uint64_t(rd()) << 32) ^ rd();
+    return x ? x : 1;
+  }();
+  return v;
+}
+
+// wall_clock64() ticks of one bounded wait: NKHIP_PEER_TIMEOUT_S seconds (default 20)
+uint64_t wait_ticks() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+    khz = 100000;  // the 100 MHz constant clock of CDNA3/4
+  const char* e = std::getenv("NKHIP_PEER_TIMEOUT_S");
+  double s = (e && *e) ? std::atof(e) : 20.0;
+  if (!(s > 0)) s = 20.0;
+  return uint64_t(s * 1e3 * double(khz));
+}
 
 struct PeerComm final : nk_comm {
   int r = 0, p = 1;
@@ -109,6 +134,7 @@ struct PeerComm final : nk_comm {
   int* err = nullptr;  // pinned host
   hipStream_t side = nullptr;  // abort writes (never queued behind a spinning collective)
   uint64_t red_tag = 0, halo_tag = 0;
+  uint64_t ticks = 0;  // wait bound (wait_ticks)
   bool connected = false, same_dev = false, any_shared = false, aborted = false;
   PeerBlob blob{};
 
@@ -137,6 +163,7 @@ struct PeerComm final : nk_comm {
     a.tag = tag;
     a.counter = counter;
     a.err = err;
+    a.wait_ticks = ticks;
     return a;
   }
 
@@ -164,8 +191,8 @@ struct PeerComm final : nk_comm {
            hipStream_t s) override {
     if (!connected || failed()) return NK_ECOMM;
     if (nx > max_nx || ny < 2) return NK_EINVAL;
-    hipLaunchKernelGGL(peer_halo_kernel, dim3(unsigned((nx + kHaloBlock - 1) / kHaloBlock)),
-                       dim3(kHaloBlock), 0, s, args(++halo_tag), v, lo, hi, ny, nx);
+    hipLaunchKernelGGL(peer_halo_kernel, dim3(unsigned(halo_blocks(nx))), dim3(kHaloBlock), 0, s,
+                       args(++halo_tag), v, lo, hi, ny, nx);
     return hipGetLastError() == hipSuccess ? NK_OK : NK_EHIP;
   }
 
@@ -236,6 +263,7 @@ int comm_create_peer(nk_comm** out, int rank, int nranks, int64_t max_nx, void* 
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
     return NK_EHIP;
   *c->err = 0;
+  c->ticks = wait_ticks();
   PeerBlob& b = c->blob;
   std::memset(&b, 0, sizeof(b));
   if (hipIpcGetMemHandle(&b.ipc, c->local) != hipSuccess) {
@@ -243,6 +271,7 @@ int comm_create_peer(nk_comm** out, int rank, int nranks, int64_t max_nx, void* 
     std::memset(&b.ipc, 0, sizeof(b.ipc));
   }
   b.ptr = reinterpret_cast<uint64_t>(c->local);
+  b.nonce = process_nonce();
   b.pid = int32_t(getpid());
   (void)hipDeviceGetAttribute(&b.bus, hipDeviceAttributePciBusId, dev);
   (void)hipDeviceGetAttribute(&b.dev, hipDeviceAttributePciDeviceId, dev);
@@ -258,6 +287,18 @@ int comm_peer_connect(nk_comm* comm, const void* handles) {
   if (!c || !handles || c->connected) return NK_EINVAL;
   const auto* blobs = static_cast<const PeerBlob*>(handles);
   if (std::memcmp(&blobs[c->r], &c->blob, sizeof(PeerBlob)) != 0) return NK_EINVAL;
+  // One process per rank.  Ranks as threads of one process share its GPU_MAX_HW_QUEUES in-order
+  // hardware queues, so a collective kernel waiting for a peer rank can sit in a queue ahead of
+  // the very launch it waits for: such a group would time out, so it is refused here.
+  auto same_process = [](const PeerBlob& x, const PeerBlob& y) {
+    return x.pid == y.pid && x.nonce == y.nonce;
+  };
+  for (int q = 0; q < c->p; ++q)
+    if (q != c->r && same_process(blobs[q], c->blob)) {
+      std::fprintf(stderr, "nkhip: peer comm ranks %d and %d are one process (one process per "
+                           "rank is required)\n", c->r, q);
+      return NK_EINVAL;
+    }
   c->base.assign(c->p, nullptr);
   c->opened.assign(c->p, false);
   for (int q1 = 0; q1 < c->p; ++q1)  // every rank sees every blob: the same answer everywhere
@@ -270,8 +311,8 @@ int comm_peer_connect(nk_comm* comm, const void* handles) {
     if (b.bytes != c->bytes) return NK_EINVAL;  // every rank built for the same group shape
     if (q != c->r && b.bus == c->blob.bus && b.dev == c->blob.dev && b.domain == c->blob.domain)
       c->same_dev = true;
-    if (b.pid == c->blob.pid) {  // this process (the rank itself, or a rank on another thread)
-      c->base[q] = reinterpret_cast<char*>(b.ptr);
+    if (q == c->r) {  // the rank itself: its own pointer (other ranks are other processes)
+      c->base[q] = c->local;
       continue;
     }
     void* ptr = nullptr;

@@ -14,6 +14,16 @@ namespace nk {
 constexpr int kMaxPeers = 64;
 constexpr int kRedMax = 256;  // values per all-reduce (the fused multi-dot: 2 nv + 3 <= 73)
 constexpr int kHaloBlock = 256;
+// Column blocks of a halo-exchange grid (peer_halo_kernel, the slab edge + halo kernel), which
+// stride over wider rows: every block of such a grid waits for flags published only once all of
+// the grid's blocks have counted in, so the grid must be able to be resident as a whole even when
+// several ranks' grids share one GPU -- at most 16 x 4 blocks of 4 waves = 256 waves per rank,
+// against 256 CUs x 32 wave slots.
+constexpr int kHaloMaxBlocks = 16;
+__host__ __device__ inline int halo_blocks(int64_t nx) {
+  const int64_t b = (nx + kHaloBlock - 1) / kHaloBlock;
+  return int(b < kHaloMaxBlocks ? (b > 0 ? b : 1) : kHaloMaxBlocks);
+}
 
 // byte offsets inside a rank's exported buffer
 constexpr int64_t kOffAbort = 0;                                  // uint64
@@ -41,6 +51,7 @@ struct PeerArgs {
   uint64_t tag;
   uint32_t* counter;  // arrival counter of the halo kernel's blocks (local, reset by the last)
   int* err;           // pinned host error word
+  uint64_t wait_ticks;  // bound of one wait, in wall_clock64() ticks (NKHIP_PEER_TIMEOUT_S)
 };
 
 __device__ __forceinline__ uint64_t* red_flag(char* b, int par, int q) {
@@ -64,39 +75,45 @@ __device__ __forceinline__ uint64_t* xflag(char* b, int P, int64_t max_nx, int p
   return reinterpret_cast<uint64_t*>(b + off_xflag(P, max_nx)) + (par * 2 + side) * x_chunks(max_nx) + ch;
 }
 
-constexpr uint64_t kSpinMax = uint64_t(1) << 27;  // polls of ~150 ns: ~20 s
-
 // Wait (one lane) until *flag == tag; false on abort (the abort word of my buffer `me`) or
 // timeout, with the error word set.  The polls are relaxed (they read past the caches, system
 // scope) and ONE acquire follows the tag: an acquire per poll would invalidate this XCD's L2 over
 // and over, under the feet of every other block on it (the fused kernel's edge bands wait while
-// the interior bands stream).
-__device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const char* me, int* err) {
+// the interior bands stream).  The bound is elapsed time on the constant-rate wall clock
+// (`ticks` of wall_clock64(), set from hipDeviceAttributeWallClockRate on the host), checked
+// every 64 polls, so it holds whatever one poll costs.
+__device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const char* me, int* err,
+                                     uint64_t ticks) {
   const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(me + kOffAbort);
-  for (uint64_t n = 0;; ++n) {
+  uint64_t t0 = 0;
+  for (uint32_t n = 0;; ++n) {
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag) {
       __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope
       return true;
     }
-    if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-        n > kSpinMax) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
+    if ((n & 63) == 0) {
+      const uint64_t now = wall_clock64();
+      if (n == 0) t0 = now;
+      if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+          now - t0 > ticks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
     }
     __builtin_amdgcn_s_sleep(4);
   }
 }
 __device__ inline bool wait_tag(const PeerArgs& a, const uint64_t* flag) {
-  return wait_flag_tag(flag, a.tag, a.base[a.rank], a.err);
+  return wait_flag_tag(flag, a.tag, a.base[a.rank], a.err, a.wait_ticks);
 }
 
 // The second half of a halo exchange, called by every block of the grid after the block wrote
-// its part of the neighbours' staging rows (thread c of a block with blockIdx.y == 0: column c):
-// the last block to arrive publishes both neighbours' flags (release, system scope), every block
-// waits for its own two flags, and the blockIdx.y == 0 blocks copy their columns of the staged
-// rows into lo / hi (2 rows of nx each).  false: a peer failed or timed out (error word set, lo / hi untouched).
-__device__ inline bool peer_halo_finish(const PeerArgs& a, int64_t c, int64_t nx, double* lo,
-                                        double* hi) {
+// its part of the neighbours' staging rows: the last block to arrive publishes both neighbours'
+// flags (release, system scope), every block waits for its own two flags, and the blockIdx.y == 0
+// blocks copy their columns -- blockIdx.x * kHaloBlock + threadIdx.x, strided by the grid's
+// columns (halo_blocks) -- of the staged rows into lo / hi (2 rows of nx each).  false: a peer
+// failed or timed out (error word set, lo / hi untouched).
+__device__ inline bool peer_halo_finish(const PeerArgs& a, int64_t nx, double* lo, double* hi) {
   const int par = int(a.tag & 1);
   const int prev = (a.rank - 1 + a.P) % a.P, next = (a.rank + 1) % a.P;
   __threadfence_system();
@@ -120,12 +137,15 @@ __device__ inline bool peer_halo_finish(const PeerArgs& a, int64_t c, int64_t nx
   __syncthreads();
   if (!ok) return false;
   __threadfence_system();
-  if (c < nx && blockIdx.y == 0) {
+  if (blockIdx.y == 0) {
     char* mine = a.base[a.rank];
-    lo[c] = stage(mine, a.P, a.max_nx, par, 0, 0)[c];
-    lo[nx + c] = stage(mine, a.P, a.max_nx, par, 0, 1)[c];
-    hi[c] = stage(mine, a.P, a.max_nx, par, 1, 0)[c];
-    hi[nx + c] = stage(mine, a.P, a.max_nx, par, 1, 1)[c];
+    const int64_t step = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; c < nx; c += step) {
+      lo[c] = stage(mine, a.P, a.max_nx, par, 0, 0)[c];
+      lo[nx + c] = stage(mine, a.P, a.max_nx, par, 0, 1)[c];
+      hi[c] = stage(mine, a.P, a.max_nx, par, 1, 0)[c];
+      hi[nx + c] = stage(mine, a.P, a.max_nx, par, 1, 1)[c];
+    }
   }
   return true;
 }

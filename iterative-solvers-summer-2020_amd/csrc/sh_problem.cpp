@@ -353,6 +353,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     A.x.max_nx = pa.max_nx;
     A.x.tag = pa.tag;
     A.x.err = pa.err;
+    A.x.wait_ticks = pa.wait_ticks;
     A.yh = stage(A.x.me, pa.P, pa.max_nx, par, 0, 0);
     A.yh_ld = pa.max_nx;
     edge_launched_ = false;

@@ -91,9 +91,12 @@ class RcclComm(Comm):
 class PeerComm(Comm):
     """Peer-memory communicator (csrc/peer.hip): every rank exports one fine-grained device
     buffer; halos and all-reduces are single small kernels that write into the peers' buffers
-    over xGMI and wait for tagged flags -- no RCCL call on the solver's stream.  Works for one
-    process per GPU, several processes on one GPU (IPC on the same device) and several ranks
-    (threads) in one process.  ``max_nx``: the widest slab row any collective will carry."""
+    over xGMI and wait for tagged flags -- no RCCL call on the solver's stream.  One PROCESS per
+    rank: one process per GPU, or several processes on one GPU (IPC on the same device).  Ranks
+    as threads of one process are refused (nk_comm_peer_connect returns NK_EINVAL): they share
+    the process's in-order hardware queues, so a collective waiting for a peer rank could sit
+    ahead of the very launch it waits for.  ``max_nx``: the widest slab row any collective will
+    carry."""
 
     def __init__(self, handle, rank, size, blob=b""):
         super().__init__(handle, rank, size)
@@ -127,8 +130,12 @@ class PeerComm(Comm):
 
 
 def peer_comms(nranks: int, max_nx: int):
-    """A peer-memory group of ``nranks`` ranks inside this process (one host thread per slab;
-    the ranks' buffers are mapped directly, no IPC)."""
+    """A peer-memory group inside this process: only a world of one (the rank is its own ring
+    neighbour; tests, bench.py --peer-self).  Several ranks need one process each
+    (PeerComm.from_torch_distributed)."""
+    if nranks != 1:
+        raise ValueError("a peer-memory group takes one process per rank: build it with "
+                         "PeerComm.from_torch_distributed in each rank's process")
     cs = [PeerComm.create(r, nranks, max_nx) for r in range(nranks)]
     blobs = [c.blob for c in cs]
     for c in cs:

@@ -13,7 +13,10 @@ Writes tests/golden/droplet_*.npz (inputs and outputs only, no reference source)
                       at the fixed step-1 mesh (:383), with Newton-iteration / F-eval counts
   droplet_pma         Q.val after loop_pma(3e-9, 5) and after loop_pma(3e-9, 400) (:589-599)
   droplet_evolve      U.new, Q.val, scale after evolve_with_PDE(1e-4, 3, 1e-2, 3e-9, 400) (2 steps)
-Run:  MPLBACKEND=Agg python tests/golden/make_golden_droplet.py
+  droplet_evolve10    config 3 over its SURVEY 8(d) length: evolve_with_PDE(1e-4, 11, 1e-2, 3e-9,
+                      400) (S = 10 steps), U.new / Q.val / dt_n / Newton its after EVERY step,
+                      recorded by wrapping the module's loop_pma (called once per step, :384)
+Run:  MPLBACKEND=Agg python tests/golden/make_golden_droplet.py [evolve10]
 """
 import contextlib
 import io
@@ -111,5 +114,49 @@ def main():
     print(log.getvalue())
 
 
+def evolve10():
+    """S = 10 steps of evolve_with_PDE from the coal init state, every step recorded."""
+    dr = load_reference()
+    d = np.loadtxt(os.path.join(REF_DIR, INIT))
+    U0, Q0 = d[:, 0].copy(), d[:, 1].copy()
+    reset(dr, U0, Q0)
+    rec = {"U": [], "Q": [], "nit": []}
+    inner = dr.loop_pma
+    real_nk = dr.newton_krylov
+    nits = [0]
+
+    def nk(*a, **kw):  # counts the Newton iterations of each step's solve
+        cb = kw.pop("callback", None)
+        nits[0] = 0
+
+        def count(x, f):
+            nits[0] += 1
+            if cb:
+                cb(x, f)
+        return real_nk(*a, callback=count, **kw)
+
+    def pma(dtmesh, loops):  # evolve_with_PDE calls it once per step, after the solve (:384)
+        rec["nit"].append(nits[0])
+        inner(dtmesh, loops)
+        rec["U"].append(dr.U.new.copy())
+        rec["Q"].append(dr.Q.val.copy())
+
+    dr.loop_pma = pma
+    dr.newton_krylov = nk
+    log = io.StringIO()
+    with contextlib.redirect_stdout(log):
+        dr.evolve_with_PDE(1e-4, 11, 1e-2, 3e-9, 400)
+    # "<it> 0.0001 * <scale> = <dt_n> . T = ..." per step (:408-409)
+    dts = [float(ln.split("=")[1].split()[0]) for ln in log.getvalue().splitlines()
+           if " * " in ln and ". T = " in ln]
+    assert len(dts) == 10 and len(rec["U"]) == 10, (len(dts), len(rec["U"]))
+    np.savez_compressed(os.path.join(OUT, "droplet_evolve10.npz"), U=np.array(rec["U"]),
+                        Q=np.array(rec["Q"]), dt=np.array(dts), nit=np.array(rec["nit"]))
+    print("dt", dts, "nit", rec["nit"])
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["evolve10"]:
+        evolve10()
+    else:
+        main()

@@ -1,0 +1,41 @@
+"""GPU: bench.py's N-GPU line produced by the driver's own command form, ``python bench.py
+--gpus N`` without a launcher (bench.py self_launch: N rank processes, rank 0's JSON line
+forwarded).  On the one-GPU box the ranks share device 0 (NKHIP_BENCH_ONE_DEVICE=1, gloo side
+channel) and run the peer-memory communicator through IPC -- the multi-process path of the
+8-GPU run minus xGMI.  Parity: the final timed step is a root of the oracle residual over the
+whole gathered grid (final_step_check, sh_scipy_nk.py:47-49) within SciPy's default f_tol."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launch_four_ranks_one_gpu():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["NKHIP_BENCH_ONE_DEVICE"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--n",
+                        "1024", "--steps", "2", "--warmup", "1", "--extra", "off", "--pmc", "off"],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=540)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["comm"] == "PeerComm", d["config"]
+    assert d["config"]["parallelism"] == "row-slab x4"
+    fc = d["final_step_check"]
+    assert fc["max_abs_residual"] <= fc["f_tol"], fc
+    ab = d["slab_exchange_ab"]
+    assert ab["edge_halo_ms_per_arnoldi"] > 0 and ab["in_kernel_ms_per_arnoldi"] > 0, ab
+    # the roofline names the dominant streaming kernel (with four ranks time-sharing one GPU the
+    # slab edge kernel's waits for the other processes are the largest kernel time: excluded)
+    assert d["value"] > 0 and d["roofline"]["kernel"] == "arnoldi_fused"

@@ -71,6 +71,24 @@ def test_two_full_steps(drop):
     assert dts[0] == 1e-4 and abs(dts[1] - 1.0102881691663517e-4) <= 1e-12
 
 
+def test_ten_full_steps_every_step(drop):
+    """Config 3 over its SURVEY 8(d) length: evolve_with_PDE(1e-4, 11, 1e-2, 3e-9, 400) = S = 10
+    steps (droplet.py:360-411), U, Q, dt_n and the Newton count checked after EVERY step against
+    the reference's own run (tests/golden/make_golden_droplet.py evolve10).  Bars as for the two
+    steps above: U within 1e-6 absolute (NK roots at f_tol = 1e-7, |U| <= ~1), Q within 1e-8
+    relative; dt_n carries the exp(-10 |U.new - U.val|) scale recursion (:411), so the roots'
+    1e-8-level differences reach it: within 1e-9 absolute (1e-5 relative; the NumPy oracle
+    lands 3e-12 from the reference); Newton its +-1."""
+    z = load_golden("droplet_evolve10")
+    for s in range(10):
+        dt = drop.step(1e-4, 3e-9, 400)
+        U, Q = drop.state()
+        assert np.abs(U.cpu().numpy() - z["U"][s]).max() <= 1e-6, s
+        assert _rel(Q, z["Q"][s]) <= 1e-8, s
+        assert abs(dt - float(z["dt"][s])) <= 1e-9, (s, dt, float(z["dt"][s]))
+        assert abs(drop.last_stats["nit"] - int(z["nit"][s])) <= 1, (s, drop.last_stats)
+
+
 def test_generic_dropin_on_droplet_residual(drop):
     """The same fixed-mesh solve through nkhip.newton_krylov with the device residual as F."""
     import nkhip

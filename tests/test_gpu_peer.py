@@ -5,17 +5,16 @@ Two ways to run the same protocol on one MI355X:
     its own buffer);
   * several PROCESSES on one GPU, the buffers mapped through IPC handles exchanged over a gloo
     torch.distributed group -- the multi-process path the 8-GPU bench runs, minus xGMI.
-Several ranks as threads of ONE process are not a supported way to run it (only the abort test
-does, with one rank idle): HIP maps the process's streams onto GPU_MAX_HW_QUEUES (4) in-order
-hardware queues, so a slab's collective kernel, waiting for a peer slab, can sit in the same
-queue ahead of the very launch it waits for.  One process per slab has its own queues.
+Several ranks as threads of ONE process are refused (nk_comm_peer_connect: NK_EINVAL): HIP maps
+the process's streams onto GPU_MAX_HW_QUEUES (4) in-order hardware queues, so a slab's
+collective kernel, waiting for a peer slab, could sit in the same queue ahead of the very launch
+it waits for.  One process per slab has its own queues.
 Parity bar as for the other slab tests: the gathered slabs equal the single-slab step to
 1e-8 max(1, |U|) at f_tol = 1e-10 (the decomposition only changes summation order).
 """
 import os
 import socket
 import sys
-import threading
 import time
 
 import numpy as np
@@ -55,41 +54,6 @@ def test_peer_world1_matches_single_slab(xk, monkeypatch):
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
 
 
-def test_peer_abort_releases_blocked_rank():
-    """nk_comm_abort's contract: rank 1 fails before its step; rank 0, already waiting in a
-    collective for it, returns NK_ECOMM (an NKError) within seconds instead of hanging."""
-    import nkhip
-    N = 64
-    comms = nkhip.peer_comms(2, N)
-    U0 = np.random.default_rng(1).standard_normal((N, N))
-    err = [None]
-    done = threading.Event()
-
-    def rank0():
-        stream = torch.cuda.Stream()
-        try:
-            with torch.cuda.stream(stream):
-                row0, ny = nkhip.slab_rows(N, 0, 2)
-                m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, comm=comms[0], ny_local=ny,
-                                         stream=stream)
-                m.step(torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda"))
-        except Exception as e:  # noqa: BLE001 - the expected failure
-            err[0] = e
-        finally:
-            done.set()
-
-    t = threading.Thread(target=rank0, daemon=True)
-    t0 = time.time()
-    t.start()
-    time.sleep(2.0)  # rank 0 is inside its first collective by now
-    comms[1].abort()
-    assert done.wait(60), "rank 0 still blocked 60 s after the abort"
-    assert isinstance(err[0], nkhip.NKError), err[0]
-    assert time.time() - t0 < 60
-    for c in comms:
-        c.close()
-
-
 # ---------------------------------------------------------------------------------------------
 # several processes on one GPU
 # ---------------------------------------------------------------------------------------------
@@ -107,16 +71,19 @@ comm = nkhip.PeerComm.from_torch_distributed(max_nx=N)
 assert comm.selftest(N), "nk_comm_selftest failed"  # the bench's check before it trusts the group
 U0 = np.random.default_rng(2020).standard_normal((N, N))
 row0, ny = nkhip.slab_rows(N, rank, world)
-m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comm, ny_local=ny)
+ftol = os.environ.get("GRID_FTOL", "1e-10")
+kw = {{}} if ftol == "default" else {{"f_tol": float(ftol)}}
+m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, comm=comm, ny_local=ny, **kw)
 U = torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda")
+del U0
 steps = int(os.environ.get("GRID_STEPS", "1"))
 for _ in range(steps):
     U = m.step(U)
 st = m.last_stats
 torch.cuda.synchronize()
 np.save(os.path.join(os.environ["OUT_DIR"], f"slab{{rank}}.npy"), U.cpu().numpy())
-print(f"rank {{rank}} nit {{st['nit']}} narn {{st['n_arnoldi']}} dev {{st['n_device_steps']}}",
-      flush=True)
+print(f"rank {{rank}} nit {{st['nit']}} narn {{st['n_arnoldi']}} dev {{st['n_device_steps']}} "
+      f"status {{st['status']}}", flush=True)
 dist.barrier()
 m.close()
 comm.close()
@@ -176,3 +143,144 @@ def test_peer_processes_match_single_slab(world, N, steps, xk, tmp_path):
         assert p.returncode == 0, o[-3000:]
     got = np.concatenate([np.load(tmp_path / f"slab{r}.npy") for r in range(world)], axis=0)
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max()), outs
+
+
+def _run_workers(tmp_path, body, world, extra_env=None, timeout=240):
+    """``world`` processes of the worker ``body`` on this GPU (gloo side channel); returns their
+    outputs after asserting every exit code is 0."""
+    import subprocess
+    script = tmp_path / "worker.py"
+    script.write_text(body.format(root=ROOT, pkg=PKG))
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OUT_DIR=str(tmp_path), LOCAL_RANK="0",
+                   **(extra_env or {}))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    return outs
+
+
+_ABORT_WORKER = r"""
+import os, sys, time
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path[:0] = [{root!r}, {pkg!r}]
+import nkhip
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+N = 64
+comm = nkhip.PeerComm.from_torch_distributed(max_nx=N)
+dist.barrier()
+if rank == 1:
+    time.sleep(2.0)  # rank 0 is inside its first collective by now
+    comm.abort()
+    print("rank 1 aborted", flush=True)
+else:
+    U0 = np.random.default_rng(1).standard_normal((N, N))
+    row0, ny = nkhip.slab_rows(N, 0, world)
+    t0 = time.time()
+    try:
+        m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, comm=comm, ny_local=ny)
+        m.step(torch.as_tensor(U0[row0:row0 + ny].copy(), device="cuda"))
+        raise SystemExit("rank 0 stepped although its peer aborted")
+    except nkhip.NKError as e:
+        dt = time.time() - t0
+        assert dt < 60, dt
+        print(f"rank 0 released after {{dt:.1f}} s: {{e}}", flush=True)
+torch.cuda.synchronize()
+comm.close()
+"""
+
+
+@pytest.mark.timeout(200)
+def test_peer_abort_releases_blocked_rank(tmp_path):
+    """nk_comm_abort's contract, across processes: rank 1 fails before its step and aborts;
+    rank 0, already waiting in a collective for it, gets NK_ECOMM (an NKError) within seconds
+    instead of hanging -- the abort word travels through the IPC-mapped buffer."""
+    outs = _run_workers(tmp_path, _ABORT_WORKER, 2, timeout=150)
+    assert "released" in outs[0] and "aborted" in outs[1], outs
+
+
+def test_peer_threads_in_one_process_refused():
+    """Two ranks of one group in one process: refused at connect (one process per rank)."""
+    import nkhip
+    with pytest.raises(ValueError):
+        nkhip.peer_comms(2, 64)
+    a = nkhip.PeerComm.create(0, 2, 64)
+    b = nkhip.PeerComm.create(1, 2, 64)
+    try:
+        with pytest.raises(nkhip.NKError):
+            a.connect([a.blob, b.blob])
+    finally:
+        a.close()
+        b.close()
+
+
+_WIDE_WORKER = r"""
+import os, sys
+import torch
+import torch.distributed as dist
+sys.path[:0] = [{root!r}, {pkg!r}]
+import nkhip
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+NX = int(os.environ["WIDE_NX"])
+comm = nkhip.PeerComm.from_torch_distributed(max_nx=NX)
+for _ in range(3):
+    assert comm.selftest(NX), "nk_comm_selftest failed"
+torch.cuda.synchronize()
+dist.barrier()
+comm.close()
+print("ok", flush=True)
+"""
+
+
+@pytest.mark.timeout(200)
+def test_peer_wide_rows_shared_gpu(tmp_path):
+    """4 processes on this GPU, 16384-column rows: the halo kernel's grid is capped
+    (kHaloMaxBlocks) and strides over the row, so it always fits the GPU as a whole although
+    every block waits for flags the last block publishes."""
+    outs = _run_workers(tmp_path, _WIDE_WORKER, 4, {"WIDE_NX": "16384"}, timeout=150)
+    assert all("ok" in o for o in outs), outs
+
+
+@pytest.mark.timeout(900)
+def test_config5_16384_eight_processes(tmp_path):
+    """BASELINE config 5 through the multi-process path the 8-GPU bench runs: a 16384^2 grid as 8
+    row slabs in 8 PROCESSES on this GPU (a ~16 GB workspace pool each, ~130 GB together), the
+    peer-memory communicator mapped through IPC with its self-test at the full row width, one
+    default-f_tol FD step from default_rng(2020) under the device-side control.  Every rank
+    reports the same Newton count; the gathered state is a root of the oracle residual over the
+    whole grid (sh_scipy_nk.py:47-49) and equals the same step solved as ONE 16384^2 slab to the
+    tolerance's scale (as test_gpu_nk.py::test_config5_16384_eight_slabs with loopback slabs)."""
+    from test_gpu_nk import _residual_rows
+    import nkhip
+    N, P = 16384, 8
+    outs = _run_workers(tmp_path, _WORKER, P, {"GRID_N": str(N), "GRID_STEPS": "1",
+                                               "GRID_FTOL": "default"}, timeout=700)
+    nits = {int(o.split(" nit ")[1].split()[0]) for o in outs}
+    assert len(nits) == 1 and all(" status 0" in o for o in outs), outs
+    U1 = np.concatenate([np.load(tmp_path / f"slab{r}.npy") for r in range(P)], axis=0)
+    U0 = np.random.default_rng(2020).standard_normal((N, N))
+    assert _residual_rows(U1, U0, 0.625, 0.01, 0.2, 1.0) <= 1.01 * np.finfo(float).eps ** (1 / 3)
+    m = nkhip.SwiftHohenberg(N=N, d=0.625 * N)
+    Us = m.step(torch.as_tensor(U0, device="cuda")).cpu().numpy()
+    nit1 = m.last_stats["nit"]
+    m.close()
+    torch.cuda.empty_cache()
+    assert abs(nit1 - nits.pop()) <= 1
+    assert float(np.abs(U1 - Us).max()) <= 1e-5 * max(1.0, float(np.abs(Us).max()))

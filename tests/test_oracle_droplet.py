@@ -76,3 +76,16 @@ def test_init_coalescing_reproduces_reference_init_file():
     u, q = D.init_coalescing()
     assert _rel(u, z["U0"]) <= 1e-11
     assert _rel(q, z["Q0"]) <= 1e-13
+
+
+def test_evolve_ten_steps_matches_reference():
+    """The oracle's evolve_with_PDE over config 3's S = 10 steps (droplet.py:360-411) against the
+    reference's own run, every step's dt_n and the final U, Q (tests/golden droplet_evolve10).
+    Both sides solve to f_tol = 1e-7 with different summation orders, and dt_n carries the
+    exp(-10 |U.new - U.val|) scale recursion (:411): measured 3e-12 (dt), 3e-8 (U), 4e-10 (Q)."""
+    z = load_golden("droplet_evolve10")
+    u0 = load_golden("droplet_init")
+    u, q, _, dts = D.evolve(u0["U0"], u0["Q0"], 10)
+    assert np.abs(np.array(dts) - z["dt"]).max() <= 1e-10
+    assert np.abs(u - z["U"][-1]).max() <= 1e-6
+    assert _rel(q, z["Q"][-1]) <= 1e-8
