@@ -7,7 +7,7 @@ loop body of the reference (sh_scipy_nk.py:56-61), on the config-4 workload: N =
 h = 0.625 (d = 0.625 N, SURVEY.md section 7 hard part 2), k = 0.2, r = 0.01, g = 1,
 U0 = default_rng(2020).standard_normal(N^2), scipy-default tolerances, FD (scipy-faithful) JVP.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]       (N > 1: starts N rank processes itself)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 N > 1: the same 4096^2 grid is cut into N row slabs (strong scaling); halo exchange and
@@ -554,23 +554,24 @@ def main():
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
         sys.exit(2)
-    # testing on one GPU: every rank on device 0 (gloo side channel, peer communicator only)
+    # testing on one GPU: every rank on device 0 (peer communicator only)
     one_device = world > 1 and os.environ.get("NKHIP_BENCH_ONE_DEVICE") == "1"
     device = 0 if one_device else local
     torch.cuda.set_device(device)
     comm = None
     use_dist = world > 1 or args.rccl_self or args.peer_self
-    coll_dev = "cpu" if one_device else "cuda"  # where torch.distributed's tensors live
+    # torch.distributed is only the side channel (IPC handle / RCCL unique-id exchange, barriers,
+    # the max over ranks of the timed region, the final gather): gloo on host tensors.  The
+    # solver's collectives run in libnkhip (peer-memory kernels, or its own RCCL communicator),
+    # and a torch NCCL group would only add its own RCCL communicator, buffers and threads.
+    coll_dev = "cpu"
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1:  # --rccl-self / --peer-self without a launcher: a world of one
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
             os.environ.setdefault("MASTER_PORT", "29531")
-        if one_device:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        dist.init_process_group("gloo")
         if args.rccl_self or (world > 1 and args.comm == "rccl" and not args.peer_self):
             comm = nkhip.RcclComm.from_torch_distributed()
         else:

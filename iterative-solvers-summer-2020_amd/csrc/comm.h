@@ -11,6 +11,8 @@
 
 #include <cstdint>
 
+#include "../../include/nkhip.h"
+
 namespace nk {
 struct PeerArgs;  // peer_dev.h
 }
@@ -22,6 +24,17 @@ struct nk_comm {
   // dev[0, nsum) summed and dev[nsum, nv) max-reduced over ranks, in place in device memory,
   // ordered on `s` (RCCL: enqueued, no host synchronisation).  Returns 0 or a negative NK_E* code.
   virtual int allreduce(double* dev, int nsum, int nv, hipStream_t s) = 0;
+  // The same, with the result also in `host` (pinned host memory) once the stream reaches it:
+  // here a D2H copy ordered after the all-reduce; the peer-memory communicator's kernel writes
+  // it itself (allreduce_writes_host: no runtime blit, and the host may poll the slot).
+  virtual int allreduce_host(double* dev, double* host, int nsum, int nv, hipStream_t s) {
+    const int rc = allreduce(dev, nsum, nv, s);
+    if (rc) return rc;
+    return hipMemcpyAsync(host, dev, sizeof(double) * nv, hipMemcpyDeviceToHost, s) == hipSuccess
+               ? NK_OK
+               : NK_EHIP;
+  }
+  virtual bool allreduce_writes_host() const { return false; }
   // lo <- rows ny_prev-2, ny_prev-1 of the previous rank, hi <- rows 0, 1 of the next rank
   // (periodic ring).  Enqueued on `s` (RCCL) or completed before return (loopback).
   virtual int halo(const double* v, double* lo, double* hi, int64_t ny, int64_t nx,

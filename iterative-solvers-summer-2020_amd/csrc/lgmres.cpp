@@ -76,8 +76,7 @@ int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bo
     rc = P_.jvp(X_, G0_, z, zs, omega_ / znorm, w);
     st_->njvp += 1;
   }
-  if (!rc) rc = P_.publish_edges(w);  // w enters the update of the next (fused) step
-  if (rc) return rc;
+  if (rc) return rc;  // (w enters the update of the next fused step: the JVP wrote its edges)
   st_->n_arnoldi += 1;
   // one pass: c_i = w.v_i (i <= j), Gram row v_j.v_i (i <= j, the diagonal is |v_j|^2), |w|^2
   VecList P;

@@ -69,6 +69,11 @@ struct StencilArgs {
   const double* znorm2 = nullptr;
   double omega = 0.0;
   double theta = 0.0;  // LINOP
+  // edge array of out0 (nk::edge_elems layout, below): written in-kernel for the pool vectors the
+  // fused Arnoldi kernel reads block halos from (TRIAL's F, the JVP's w), so no edge_gather pass
+  // follows them; rows e_row0.. of an e_ny-row field (a row-range launch of a slab)
+  double* E0 = nullptr;
+  int64_t e_ny = 0, e_row0 = 0;
   bool rev = false;    // set by stencil_launch (traversal_reverse)
   bool nt_p0 = false;  // set by stencil_launch: non-temporal loads of the point-wise input
 };

@@ -315,7 +315,9 @@ bool poll_enabled() {
 }  // namespace
 
 int Engine::wait_results(int slot, int nv) {
-  if (comm || !poll_enabled()) return sync();
+  // the slots are written by a kernel (one GPU: the reduction; peer-memory slabs: the all-reduce)
+  // unless the communicator's result comes back by a runtime copy
+  if ((comm && !comm->allreduce_writes_host()) || !poll_enabled()) return sync();
   volatile uint64_t* h = reinterpret_cast<volatile uint64_t*>(hres_ + slot);
   for (int k = 0; k < nv; ++k) {
     for (int64_t spins = 0; h[k] == kUnset; ++spins) {
@@ -345,7 +347,9 @@ int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot, bool host_cop
   if (slot < 0 || slot + nv > kReduceSlots) return NK_EINVAL;
   // any communicator (also a world of one) takes the all-reduce path
   const bool multi = comm != nullptr;
-  if (!multi) {  // the kernel fills these pinned slots; wait_results() polls for them
+  // a kernel fills these pinned slots (the reduction on one GPU, the peer all-reduce on slabs);
+  // wait_results() polls for them
+  if (!multi || (host_copy && comm->allreduce_writes_host())) {
     uint64_t* h = reinterpret_cast<uint64_t*>(hres_ + slot);
     for (int k = 0; k < nv; ++k) h[k] = kUnset;
     std::atomic_thread_fence(std::memory_order_release);
@@ -355,12 +359,8 @@ int Engine::reduce_async(int64_t nblk, int nsum, int nv, int slot, bool host_cop
                                multi ? nullptr : hres_ + slot, s);
   });
   if (rc || !multi) return rc;
-  rc = comm->allreduce(dres_ + slot, nsum, nv, s);
-  if (rc || !host_copy) return rc;
-  return hipMemcpyAsync(hres_ + slot, dres_ + slot, sizeof(double) * nv, hipMemcpyDeviceToHost,
-                        s) == hipSuccess
-             ? NK_OK
-             : NK_EHIP;
+  if (!host_copy) return comm->allreduce(dres_ + slot, nsum, nv, s);
+  return comm->allreduce_host(dres_ + slot, hres_ + slot, nsum, nv, s);
 }
 
 int Engine::reduce(int64_t nblk, int nsum, int nv, double* out) {
@@ -599,8 +599,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
   // its trial output (no separate copy pass)
   int rc = P_.set_x0(x_in);
   double red[3];
-  if (!rc) rc = P_.eval(x_in, x_in, 0.0, X_, Fx_, G0_, red);
-  if (!rc) rc = P_.publish_edges(Fx_);  // V_0 of every Arnoldi process of this iterate
+  if (!rc) rc = P_.eval(x_in, x_in, 0.0, X_, Fx_, G0_, red);  // (Fx_ = V_0: edges written)
   if (rc) return rc;
   st_->nfev = 1;
   fx_norm_ = std::sqrt(red[0]);
@@ -643,8 +642,7 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
     std::swap(X_, Xt_);
     std::swap(Fx_, Ft_);
     std::swap(G0_, Gt_);
-    rc = P_.set_x0(X_);
-    if (!rc) rc = P_.publish_edges(Fx_);
+    rc = P_.set_x0(X_);  // (Fx_, the accepted trial's F, came with its edge array)
     if (rc) break;
     omega_ = rdiff_ * std::max(1.0, xmax) / std::max(1.0, fmax);  // jacobian.update
     const double eta_A = gamma * fnorm_new * fnorm_new / (fx_norm_ * fx_norm_);

@@ -246,7 +246,9 @@ struct Problem {
   }
   // ctl of fused_step (device-side Arnoldi control, nk_kernels.h ArnoldiArgs): c, tau, zs and sc
   // come from the device parameter block ctl, and the step does nothing when its halt entry is set.
-  // v (a pool vector) may enter the update of a later fused step: refresh its edge array
+  // v (a pool vector) may enter the update of a later fused step: refresh its edge array.
+  // eval()'s F and jvp()'s w come with fresh edge arrays (written by the pass itself); the solver
+  // calls this after the other producers of update entries (its in-place combinations).
   virtual int publish_edges(const double* /*v*/) { return NK_OK; }
   // The last `count` fused steps were no-ops (queued past a step the device control handed
   // back): take their launches out of the kernel profile (Engine::void_last).

@@ -45,8 +45,9 @@
 namespace nk {
 namespace {
 
+// host (optional, pinned): the result is written there too (Engine::reduce_async's host slot)
 __global__ void __launch_bounds__(kRedMax) peer_allreduce_kernel(const PeerArgs a, double* dev,
-                                                                 int nsum, int nv) {
+                                                                 double* host, int nsum, int nv) {
   const int t = threadIdx.x;
   const int par = int(a.tag & 1);
   const double v = (t < nv) ? dev[t] : 0.0;
@@ -72,6 +73,7 @@ __global__ void __launch_bounds__(kRedMax) peer_allreduce_kernel(const PeerArgs 
       acc = (t < nsum) ? acc + x : nmax(acc, x);
     }
     dev[t] = acc;
+    if (host) host[t] = acc;
   }
 }
 
@@ -168,13 +170,17 @@ struct PeerComm final : nk_comm {
   }
 
   int allreduce(double* dev, int nsum, int nv, hipStream_t s) override {
+    return allreduce_host(dev, nullptr, nsum, nv, s);
+  }
+  int allreduce_host(double* dev, double* host, int nsum, int nv, hipStream_t s) override {
     if (!connected || failed()) return NK_ECOMM;
     if (nv <= 0) return NK_OK;
     if (nv > kRedMax) return NK_EINVAL;
     hipLaunchKernelGGL(peer_allreduce_kernel, dim3(1), dim3(kRedMax), 0, s, args(++red_tag), dev,
-                       nsum, nv);
+                       host, nsum, nv);
     return hipGetLastError() == hipSuccess ? NK_OK : NK_EHIP;
   }
+  bool allreduce_writes_host() const override { return true; }
 
   bool take_allreduce(PeerArgs* out, int nv) override {
     if (!connected || failed() || nv < 1 || nv > kRedMax) return false;

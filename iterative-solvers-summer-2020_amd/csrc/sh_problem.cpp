@@ -99,6 +99,7 @@ StencilArgs sub_args(const StencilArgs& A, int64_t r0, int64_t r1) {
   B.a = sub_field(A.a, r0, r1, A.ny, A.nx);
   B.b = sub_field(A.b, r0, r1, A.ny, A.nx);
   const int64_t off = r0 * A.nx;
+  B.e_row0 = A.e_row0 + r0;
   if (A.p0) B.p0 = A.p0 + off;
   if (A.out0) B.out0 = A.out0 + off;
   if (A.out1) B.out1 = A.out1 + off;
@@ -183,6 +184,7 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   A.out2 = xt;
   A.c = c_;
   A.partial = E_.partial();
+  set_edges(&A, F);
   int64_t nblk = 0;
   int rc = E_.launch(K_TRIAL, stencil_bytes_per_point(SMode::TRIAL, xt != nullptr) * ny_ * nx_,
                      [&] { return stencil_launch(SMode::TRIAL, A, E_.s, &nblk); });
@@ -197,6 +199,7 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
   A.nx = nx_;
   A.c = c_;
   A.out0 = w;
+  set_edges(&A, w);
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
     A.a = field(z, hz_);
     A.alpha = zs;
@@ -218,6 +221,7 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   A.nx = nx_;
   A.c = c_;
   A.out0 = w;
+  set_edges(&A, w);
   A.znorm2 = znorm2;
   A.omega = omega;
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
@@ -394,6 +398,15 @@ void SHProblem::void_fused_steps(int count) {
   E_.void_last(K_ARNOLDI, count);
   if (dist() && edge_launched_) E_.void_last(K_ARN_EDGE, count);
   if (last_split_) E_.void_last(K_ARN_SLAB, count);
+}
+
+// The edge array of a stencil pass's output, written by the pass itself (when the fused kernel
+// will read block halos from it): TRIAL's F becomes V_0, the JVP's w the next update entry.
+void SHProblem::set_edges(StencilArgs* A, const double* out) const {
+  if (!has_fused(1)) return;
+  A->E0 = E_.edges(out);
+  A->e_ny = ny_;
+  A->e_row0 = 0;
 }
 
 int SHProblem::publish_edges(const double* v) {

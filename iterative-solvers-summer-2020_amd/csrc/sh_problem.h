@@ -31,6 +31,7 @@ class SHProblem final : public Problem {
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
   int publish_edges(const double* v) override;
+  void set_edges(StencilArgs* A, const double* out) const;
   void void_fused_steps(int count) override;
 
  private:

@@ -282,6 +282,16 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
       if (active && it < nrows) {
         const int64_t o = r * nx + cc;
         *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
+        if (A.E0) {  // the edge array: E[(b e_ny + row) 4 + 0..3] = columns B-2, B-1, B, B+1
+          const int64_t er = A.e_row0 + r;
+          const double2 ev = make_double2(res[0].o0, res[1].o0);
+          if (cc % kEdgeW == 0)
+            *reinterpret_cast<double2*>(A.E0 + ((cc / kEdgeW) * A.e_ny + er) * 4 + 2) = ev;
+          if ((cc + 2) % kEdgeW == 0 || cc + 2 == nx) {
+            const int64_t b = (cc + 2 == nx) ? 0 : (cc + 2) / kEdgeW;
+            *reinterpret_cast<double2*>(A.E0 + (b * A.e_ny + er) * 4) = ev;
+          }
+        }
         if constexpr (M == SMode::TRIAL) {
           *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
           if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
@@ -420,6 +430,7 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     else
       hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY, int(gx), int(gy));
   } else {
+    if (A.E0) return hipErrorInvalidValue;  // edge arrays come with the march path only
     const int64_t n = A.nx * A.ny;
     const int64_t g = (n + 255) / 256;
     if (nblk) *nblk = g;
