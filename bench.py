@@ -179,6 +179,16 @@ def config2_lap5(n=1024, reps=200):
     b.record()
     torch.cuda.synchronize()
     us = a.elapsed_time(b) * 1e3 / reps
+    # the kernel alone: an event pair around each launch (no inter-launch gap in the average)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record()
+        nkhip.lap5_apply(v, 1 / h ** 2, out=y)
+        e1.record()
+    torch.cuda.synchronize()
+    k_us = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e3 / reps
+    k_gbs = 16 * n * n / (k_us * 1e-6) / 1e9
     err = float(np.abs(y.cpu().numpy().reshape(-1) - sh_oracle.lap5(v_np, n, n, 1 / h ** 2)).max())
     L = sh_oracle.csr_lap(n, h)
     best = 1e9
@@ -189,7 +199,15 @@ def config2_lap5(n=1024, reps=200):
     return {"workload": f"lap5_{n}x{n}_fp64", "avg_us_per_launch_incl_gap": round(us, 2),
             "alg_GBps": round(16 * n * n / (us * 1e-6) / 1e9, 1), "max_abs_err_vs_oracle": err,
             "cpu_scipy_csr_ms": round(best * 1e3, 3),
-            "note": "back-to-back launches; the per-kernel duration is in profiles/*_summary.md"}
+            "roofline": {"kernel": "march_kernel<LAP5>", "bound": "hbm",
+                         "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(k_gbs / HBM_PEAK_GBS, 4), "avg_us": round(k_us, 2),
+                         "alg_bytes_per_launch": 16 * n * n, "launches": reps,
+                         "mall_resident": True,
+                         "note": "HIP event pair around each launch; the 16.8 MB working set "
+                                 "(v, y) stays in the 256 MB Infinity Cache between launches, "
+                                 "so HBM is not what bounds it"},
+            "note": "back-to-back launches; rocprofv3 durations in profiles/r02_config2.md"}
 
 
 def config3_droplet(steps=5, cpu_steps=2):
@@ -504,18 +522,24 @@ def self_launch(n):
 
 
 def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
-    """N > 1, after the timed region: the two slab-exchange variants of the fused Arnoldi step,
-    alternating one time step each (``rounds`` of each), as ms per Arnoldi step (max over ranks
-    of each step's wall time ÷ its Arnoldi steps).  edge_halo: the default -- a 4-row edge kernel
-    that exchanges u on the slab's edge rows, then the fused pass; in_kernel: the fused pass's
-    edge bands exchange them themselves (NKHIP_SLAB_XK=2; =1 when the ranks share a GPU), the
-    interior bands never wait.  Returns (record, a, b) with the trajectory advanced."""
-    old = os.environ.get("NKHIP_SLAB_XK")
-    acc = {"edge_halo": [0.0, 0], "in_kernel": [0.0, 0]}
+    """N > 1, after the timed region: the slab paths of the fused Arnoldi step, rotating one time
+    step each (``rounds`` of each), as ms per Arnoldi step (max over ranks of each step's wall
+    time / its Arnoldi steps).  pushed (the default): every producer writes its edge rows into the
+    neighbours' halo slots, the fused pass forms u on its halo rows itself, nothing is exchanged
+    in between; edge_halo (NKHIP_SLAB_PUSH=0): a 4-row edge kernel exchanges u on the slab's edge
+    rows before the fused pass; in_kernel (NKHIP_SLAB_XK=2, =1 when the ranks share a GPU): the
+    fused pass's edge bands exchange them themselves.  Returns (record, a, b), the trajectory
+    advanced."""
+    names = ("pushed", "edge_halo", "in_kernel")
+    env = {"pushed": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0"},
+           "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0"},
+           "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2"}}
+    old = {k_: os.environ.get(k_) for k_ in ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK")}
+    acc = {n_: [0.0, 0] for n_ in names}
     try:
-        for i in range(2 * rounds):
-            name = "edge_halo" if i % 2 == 0 else "in_kernel"
-            os.environ["NKHIP_SLAB_XK"] = ("1" if one_device else "2") if i % 2 else "0"
+        for i in range(len(names) * rounds):
+            name = names[i % len(names)]
+            os.environ.update(env[name])
             dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -527,13 +551,14 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
             acc[name][1] += model.last_stats["njvp"]
             a, b = b, a
     finally:
-        if old is None:
-            os.environ.pop("NKHIP_SLAB_XK", None)
-        else:
-            os.environ["NKHIP_SLAB_XK"] = old
+        for k_, v in old.items():
+            if v is None:
+                os.environ.pop(k_, None)
+            else:
+                os.environ[k_] = v
     rec = {f"{k_}_ms_per_arnoldi": round(1e3 * v[0] / max(v[1], 1), 4) for k_, v in acc.items()}
     rec.update({"steps_each": rounds, "arnoldi_steps": {k_: v[1] for k_, v in acc.items()},
-                "what": "alternating time steps after the timed region; max over ranks of each "
+                "what": "rotating time steps after the timed region; max over ranks of each "
                         "step's wall time / its Arnoldi steps"})
     return rec, a, b
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstddef>
 #include <cmath>
 
 #include "nk_device.h"
@@ -117,11 +118,23 @@ __device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, doub
     return;
   }
   const double gj = (lane < j) ? sig_j * sig * rg : 0.0;  // gram[j][lane]
-  // Gram rows 0..j (k < row) in LDS for the column sweep (one wave: LDS keeps its order)
+  // Gram rows 0..j (k < row) in LDS for the column sweep (one wave: LDS keeps its order).  Every
+  // load is issued before the first LDS store (a fixed, unrolled count): one memory latency for
+  // the whole matrix instead of one per 64 entries.
   __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  for (int q = lane; q < np * np; q += 64) {
-    const int r = q / np, k = q % np;
-    if (k < r && r < j) G[r][k] = S->gram[r][k];
+  {
+    constexpr int kG = ((kArnMaxNV + 1) * (kArnMaxNV + 1) + 63) / 64;
+    double gl[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      const int q = lane + 64 * i, r = q / np, k = q % np;
+      gl[i] = (q < np * np && k < r && r < j) ? S->gram[r][k] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      const int q = lane + 64 * i, r = q / np, k = q % np;
+      if (q < np * np && k < r && r < j) G[r][k] = gl[i];
+    }
   }
   if (lane < j) G[j][lane] = gj;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -177,9 +190,32 @@ __device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, doub
   if (lane == 0) __hip_atomic_store(status + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// up > 0: first copy the host's pinned loop state H to S (the fields before R, and the Gram rows
+// 0 .. up-2) -- the entry of a run of device steps, which would otherwise take two runtime blits
+// (H is mapped device-visible memory).  All loads are issued before the first store.
+__device__ void upload_state(ArnCtlState* S, const ArnCtlState* H, int rows) {
+  const int lane = threadIdx.x & 63;
+  constexpr int kHead = int(offsetof(ArnCtlState, R) / 8);  // 8-B words before R
+  constexpr int kRow = kMaxVec + 1;                          // doubles per Gram row
+  constexpr int kI = (kHead + 63) / 64;
+  const uint64_t* h = reinterpret_cast<const uint64_t*>(H);
+  uint64_t* d = reinterpret_cast<uint64_t*>(S);
+  uint64_t v[kI];
+#pragma unroll
+  for (int i = 0; i < kI; ++i) v[i] = (lane + 64 * i < kHead) ? h[lane + 64 * i] : 0;
+#pragma unroll
+  for (int i = 0; i < kI; ++i)
+    if (lane + 64 * i < kHead) d[lane + 64 * i] = v[i];
+  const double* hg = &H->gram[0][0];
+  double* dg = &S->gram[0][0];
+  for (int q = lane; q < rows * kRow; q += 64) dg[q] = hg[q];
+  __threadfence();  // the state before the control reads it (this wave, another lane's stores)
+}
+
 __global__ void __launch_bounds__(64) arn_ctl_kernel(ArnCtlState* S, ArnCtlState* H,
                                                      const double* red, double* red_host,
-                                                     double* prm, uint32_t* status, int t) {
+                                                     double* prm, uint32_t* status, int t, int up) {
+  if (up > 0) upload_state(S, H, up - 1);
   ctl_body(S, H, red, red_host, prm, status, t);
 }
 
@@ -235,10 +271,11 @@ __global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
 }  // namespace
 
 hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
-                          double* prm, uint32_t* status, int t, hipStream_t s) {
-  if (!S || !H || !red || !prm || !status || t < 0 || t > kMaxVec) return hipErrorInvalidValue;
+                          double* prm, uint32_t* status, int t, hipStream_t s, int upload_rows) {
+  if (!S || !H || !red || !prm || !status || t < 0 || t > kMaxVec || upload_rows > kMaxVec + 1)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(arn_ctl_kernel, dim3(1), dim3(64), 0, s, S, H, red, red_host, prm, status,
-                     t);
+                     t, upload_rows < 0 ? 0 : upload_rows + 1);
   return hipGetLastError();
 }
 

@@ -341,6 +341,91 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the staged rows, for every thread of the block
 }
 
+// ------------------------------------------------------------------------------------------
+// Pushed halo rows (row slabs over the peer-memory communicator, A.hs_ld > 0).  A slab's stencil
+// needs u on the neighbours' two edge rows, and u of a row is the update sum over the entries
+// [V_0 .. V_{nv-1}, w] (or z) of that row -- entries the neighbours produced in EARLIER launches.
+// So every producer of an entry writes the entry's own edge rows into its ring neighbours' halo
+// slots as a by-product (this kernel for its outputs v and w', the stencil passes and
+// combinations through push_rows_launch), with a system-scope fence and no flag: the all-reduce
+// that every rank passes between producing an entry and the next fused launch (the device
+// control's, or the host path's) orders the writes before this launch on every rank, and a slot
+// is rewritten only when its pool vector gets new content, steps after its last reader (the same
+// all-reduces order that).  Here the blocks of the first band compute u on rows -2, -1 and those
+// of the last band on rows ny, ny+1 from the slots -- their own columns and the two halo columns
+// either side, in the update's summation order (edge_u, bitwise the owner's v) -- into A.yh, then
+// march as with exchanged halo rows.  No exchange runs between the control and this launch, and
+// no block waits for another rank.  (A halo column shared with the neighbouring block is written
+// by both with the same bits.)
+template <int NV, int KMAX>
+__device__ void slab_push_prologue(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW,
+                                   int h0, const double* cst, double a_tau) {
+  const int64_t nx = A.nx, ld = A.hs_ld;
+  const bool first = band == 0, last = band == int64_t(A.nbands) - 1;
+  double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
+  constexpr int NE = NV + 1;
+  const int64_t ncol = BW + 4;  // columns B0-2 .. B0+BW+1 of the two halo rows
+  const int64_t nb = blockDim.x;
+  for (int side = 0; side < 2; ++side) {
+    if (side == 0 ? !first : !last) continue;
+    // KMAX (row, column) items per thread (2 ncol <= KMAX blockDim for the layout), entry-major
+    // so that every item's loads are in flight together: one memory latency
+    int64_t off[KMAX], yo[KMAX];
+    bool on[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int64_t i = threadIdx.x + k * nb;
+      on[k] = i < 2 * ncol;
+      const int64_t rr = (i >= ncol) ? 1 : 0;
+      const int64_t j = ((B0 - 2 + (i - rr * ncol)) % nx + nx) % nx;
+      const int64_t hrow = 2 * side + rr;  // slot / yh row: 0, 1 = rows -2, -1; 2, 3 = ny, ny+1
+      off[k] = on[k] ? CI(hrow * ld + j, 4 * ld) : 0;
+      yo[k] = on[k] ? CI(hrow * nx + j, 4 * nx) : 0;
+    }
+    double u[KMAX];
+    if (A.z) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) u[k] = A.HS[NV + 1][off[k]];
+    } else {
+      double p0[KMAX], p1[KMAX];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) p0[k] = p1[k] = 0.0;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const double cf = (e < NV) ? cst[e] : a_tau;
+        const bool even = (h0 > 0) ? (e < h0) : ((e & 1) == 0);
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+          const double x = A.HS[e][off[k]];
+          if (even)
+            p0[k] = __builtin_fma(cf, x, p0[k]);
+          else
+            p1[k] = __builtin_fma(cf, x, p1[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) u[k] = p0[k] + p1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (on[k]) yh[yo[k]] = u[k];
+  }
+  __threadfence_block();
+  __syncthreads();
+}
+
+// v (or w') of own row q into the neighbours' halo slots when q is one of the slab's edge rows
+// (ps[0]: the previous rank's slot, rows 2, 3 <- rows 0, 1; ps[1]: the next rank's, rows 0, 1 <-
+// rows ny-2, ny-1); `st`: this lane stores row q (wave-uniform row, per-lane column)
+__device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int64_t q,
+                                              int64_t ny, int64_t col, bool st, dv2 val) {
+  const bool top = q < 2, bot = q >= ny - 2;
+  if (!(st && (top || bot))) return;
+  double* d = top ? ps[0] + (2 + q) * ld : ps[1] + (q - (ny - 2)) * ld;
+  ARN_CHK(col + 1 < ld);
+  *reinterpret_cast<dv2*>(d + col) = val;
+}
+
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
 //   [V_0 .. V_{NV-1}, w, x0, (z)]
@@ -691,6 +776,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
                                            CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
+    if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)  // wave-uniform
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
                                              st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
@@ -730,6 +816,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
                                            CO((in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB, nelem),
                                            0, 0);
+    if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in && hf == 0, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
                                              (in && hf == 0) ? eoff(r) : kOOB, 0, 0);
@@ -763,6 +850,9 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   };
 
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau);  // uniform per block
+  const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
+  // (2 (BW + 4) <= 3 blockDim: 128- and 256-column blocks of 2 and 4 waves)
+  if (edge_band) slab_push_prologue<NV, 3>(A, band, B0, BW, 0, cst, a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
     // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
@@ -811,6 +901,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
   }
 
+  if (edge_band) __threadfence_system();  // the pushed edge rows, before the kernel ends
   // one partial per wave: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']; entry 2k + hf of
   // load k is summed over its half (width-32 butterflies)
 #pragma unroll
@@ -1119,6 +1210,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     const bool st = own && q >= r0 && q < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
                                            CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
+    if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
                                              st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
@@ -1153,6 +1245,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
                                            CO(in ? uint32_t((r * nx + col) * 8) : kOOB, nelem), 0, 0);
+    if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
                                              in ? eoff(r) : kOOB, 0, 0);
@@ -1182,6 +1275,9 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   };
 
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau);  // uniform per block
+  const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
+  // (2 (BW + 4) <= 5 blockDim: 512-column blocks of 4 waves)
+  if (edge_band) slab_push_prologue<NV, 5>(A, band, B0, BW, NV + 1, cst, a_tau);
   if (nrows > 0) {
     Slot P[2];
     load(P[0], r0 - 2);
@@ -1221,6 +1317,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
   }
 
+  if (edge_band) __threadfence_system();  // the pushed edge rows, before the kernel ends
   wave_sum<NV + 3>(aw);
   wave_sum<NV>(ag);
   if (lane == 0) {

@@ -17,6 +17,17 @@ namespace nk {
 struct PeerArgs;  // peer_dev.h
 }
 
+// Halo slots of the pushed-halo-rows path (peer-memory communicator): this rank's slot region
+// and its ring neighbours' (mapped peer memory); slot q = 4 rows of `ld` doubles at base + 4 q ld
+// (rows 0, 1: the previous rank's last two rows of pool vector q, rows 2, 3: the next rank's
+// first two).
+struct nk_halo_slots {
+  double* mine = nullptr;
+  double* prev = nullptr;
+  double* next = nullptr;
+  int64_t ld = 0, count = 0;
+};
+
 struct nk_comm {
   virtual ~nk_comm() = default;
   virtual int rank() const = 0;
@@ -59,6 +70,10 @@ struct nk_comm {
   // rank must take the same sequence.  false: not available (the caller uses allreduce / halo).
   virtual bool take_allreduce(nk::PeerArgs* /*out*/, int /*nv*/) { return false; }
   virtual bool take_halo(nk::PeerArgs* /*out*/, int64_t /*nx*/) { return false; }
+  // The halo slots, for one stepper at a time (`owner`); false: none (not the peer-memory
+  // communicator, or another stepper holds them).  release_slots hands them back.
+  virtual bool claim_slots(const void* /*owner*/, nk_halo_slots* /*out*/) { return false; }
+  virtual void release_slots(const void* /*owner*/) {}
 };
 
 namespace nk {

@@ -72,6 +72,7 @@ int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bo
   } else if (znorm == 0.0) {  // KrylovJacobian.matvec: a zero vector maps to zero, no F call
     rc = E_.launch(K_COPY, 8.0 * n,
                    [&] { return hipMemsetAsync(w, 0, sizeof(double) * n, E_.s); });
+    if (!rc) rc = P_.publish_edges(w);  // (not a stencil output: its edges, its pushed rows)
   } else {  // sc = omega / |v| with v = zs z (_nonlin.py:1505-1507)
     rc = P_.jvp(X_, G0_, z, zs, omega_ / znorm, w);
     st_->njvp += 1;
@@ -401,13 +402,9 @@ int NewtonKrylov::device_steps() {
   volatile uint32_t* st = status_;
   for (int t = t0; t < S.m && t < kMaxVec + 2; ++t) st[t] = 0;
   std::atomic_thread_fence(std::memory_order_release);
-  // the state the control reads: everything before R, and the Gram rows of the earlier steps.
+  // the state the control reads -- everything before R, and the Gram rows of the earlier steps
+  // -- is copied from hS_ by the first control launch itself (arn_ctl_launch upload_rows = t0).
   // From here the device writes every committed value into hS_ as well (no read-back).
-  if (hipMemcpyAsync(dS_, hS_, offsetof(ArnCtlState, R), hipMemcpyHostToDevice, E_.s) !=
-          hipSuccess ||
-      (t0 > 0 && hipMemcpyAsync(&dS_->gram[0][0], &S.gram[0][0], sizeof(S.gram[0]) * t0,
-                                hipMemcpyHostToDevice, E_.s) != hipSuccess))
-    return NK_EHIP;
 
   const bool one = E_.comm == nullptr;  // no all-reduce: the reduction carries the control
   struct Rot {
@@ -421,11 +418,11 @@ int NewtonKrylov::device_steps() {
   // the control of step t on the (all-reduced) multi-dot results in its slot
   // the control of step t on the (all-reduced) multi-dot results in its slot; `copy`: the
   // results also to the host slot (the all-reduce path leaves out its own D2H copy)
-  auto control = [&](int t, bool copy) {
+  auto control = [&](int t, bool copy, int upload_rows = -1) {
     const int slot = Engine::slot_mdot(t);
     return E_.launch(K_CTL, 0.0, [&] {
       return arn_ctl_launch(dS_, hS_, E_.dres(slot), copy ? E_.hres_mut(slot) : nullptr, prm_,
-                            status_, t, E_.s);
+                            status_, t, E_.s, upload_rows);
     });
   };
   // the fused step nv = t + 1 with the parameters control t writes, its reduction into the slot
@@ -491,7 +488,8 @@ int NewtonKrylov::device_steps() {
   };
   // one fused step queued beyond the one whose control is awaited, so the stream never waits
   // for the host; a step handed back leaves at most one launch pair behind that does nothing
-  int rc = control(t0, false);  // step t0's results came through the host's reduce_async
+  // step t0's results came through the host's reduce_async; this launch uploads the state
+  int rc = control(t0, false, t0);
   int next = t0;  // the next fused step to queue
   if (!rc) rc = issue(next++);
   int t = t0;

@@ -73,6 +73,11 @@ struct StencilArgs {
   // fused Arnoldi kernel reads block halos from (TRIAL's F, the JVP's w), so no edge_gather pass
   // follows them; rows e_row0.. of an e_ny-row field (a row-range launch of a slab)
   double* E0 = nullptr;
+  double* E2 = nullptr;  // ... of out2 (TRIAL's x + alpha p: the next Newton iterate)
+  // edge arrays of the stencil fields a and b (same geometry): the block's side columns of an
+  // own row come from them (four rows per line) instead of the neighbouring blocks' lines
+  const double* Ea = nullptr;
+  const double* Eb = nullptr;
   int64_t e_ny = 0, e_row0 = 0;
   bool rev = false;    // set by stencil_launch (traversal_reverse)
   bool nt_p0 = false;  // set by stencil_launch: non-temporal loads of the point-wise input
@@ -193,6 +198,18 @@ struct ArnoldiArgs {
   const double* yh = nullptr;
   int64_t yh_ld = 0;               // row stride of yh (0: nx)
   SlabX x{};                       // in-kernel slab exchange (yh = this rank's staging rows)
+  // Pushed halo rows (row slabs over the peer-memory communicator, hs_ld > 0; arnoldi.hip
+  // "Pushed halo rows"): every producer of an update entry wrote that vector's edge rows into its
+  // ring neighbours' halo slots (kHaloRows rows of hs_ld per pool vector: rows 0, 1 = the previous
+  // rank's last two rows, 2, 3 = the next rank's first two), before an all-reduce this launch
+  // follows; the edge bands compute u on the halo rows from the slots into yh (rows of nx)
+  // themselves, so no exchange runs between the control and this launch.
+  const double* HS[kArnMaxNV + 2] = {};  // this rank's slots of V_0..V_{nv-1}, w, (z)
+  int64_t hs_ld = 0;
+  // this launch's outputs into the neighbours' slots: [0] the previous rank's slot of out_v (its
+  // rows 2, 3 <- my rows 0, 1), [1] the next rank's slot of out_v (its rows 0, 1 <- my rows
+  // ny-2, ny-1), [2], [3] the same for out_w
+  double* PS[4] = {};
   double* partial = nullptr;       // [(2 nv + 3)][pstride], this launch's columns from pcol0
   int64_t partial_cap = 0;         // doubles available at partial
   // rows [r_begin, r_end) of the slab are computed (r_end < 0: ny); rows outside are read only
@@ -241,6 +258,11 @@ hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
 hipError_t arnoldi_edge_halo_launch(const ArnoldiArgs& A, const PeerArgs& pa, double* yh,
                                     hipStream_t s);
 int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset);
+// Pushed halo rows (peer.hip): v's rows 0, 1 -> rows 2, 3 of prev_slot and rows ny-2, ny-1 ->
+// rows 0, 1 of next_slot (the ring neighbours' halo slots of v's pool vector, row stride ld,
+// peer memory), then a system-scope fence; nothing waits (the next all-reduce orders it).
+hipError_t push_rows_launch(const double* v, double* prev_slot, double* next_slot, int64_t ny,
+                            int64_t nx, int64_t ld, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Device-side Arnoldi control (arnctl.hip, lgmres.cpp).  The loop state of one LGMRES call: the
@@ -282,8 +304,11 @@ constexpr int kCtlPrm = kArnMaxNV + 4;
 // set.
 // red_host (optional, pinned): the kernel also copies `red` there (the host reads it when the
 // step is handed back; saves the all-reduce path its D2H copy per step).
+// upload_rows >= 0: the launch first copies H's fields before R and its Gram rows
+// 0 .. upload_rows-1 into S itself (the entry of a run of device steps; no runtime copy).
 hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
-                          double* prm, uint32_t* status, int t, hipStream_t s);
+                          double* prm, uint32_t* status, int t, hipStream_t s,
+                          int upload_rows = -1);
 // The same preceded by the reduction of the fused step's partials (one GPU: no all-reduce in
 // between) in one launch: result[k] = sum_b partial[k nblk + b] for k < nval (and result_host,
 // pinned), then the last block to finish runs the control of step t on result.

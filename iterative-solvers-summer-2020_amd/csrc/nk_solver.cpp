@@ -33,7 +33,7 @@ const char* kind_name(int kind) {
                                          "krylov_mdot", "krylov_combo", "reduce_final", "copy",
                                          "halo", "user_F", "axpby", "arnoldi_fused",
                                          "arnoldi_edge", "edge_gather", "arnoldi_slab_edges",
-                                         "arnoldi_ctl"};
+                                         "arnoldi_ctl", "halo_push"};
   return (kind >= 0 && kind < K_NKINDS) ? names[kind] : "?";
 }
 
@@ -224,6 +224,25 @@ int Engine::alloc(int count, std::vector<double*>* out, void* external, int64_t 
   return NK_OK;
 }
 
+int64_t Engine::pool_index(const double* v) const {
+  if (!pool_ || !v || v < pool_) return -1;
+  const int64_t off = v - pool_;
+  if (off % npad != 0 || off / npad >= pool_count_) return -1;
+  return off / npad;
+}
+
+void Engine::mark_edges(const double* v) {
+  const int64_t q = pool_index(v);
+  if (q < 0 || !epool_) return;
+  if (ekept_.size() < size_t(pool_count_)) ekept_.assign(pool_count_, 0);
+  ekept_[q] = 1;
+}
+
+bool Engine::edges_kept(const double* v) const {
+  const int64_t q = pool_index(v);
+  return q >= 0 && size_t(q) < ekept_.size() && ekept_[q] != 0;
+}
+
 double* Engine::edges(const double* v) const {
   if (!epool_ || !v || v < pool_) return nullptr;
   const int64_t off = v - pool_;
@@ -234,6 +253,7 @@ double* Engine::edges(const double* v) const {
 int Engine::gather_edges(const double* v) {
   double* e = edges(v);
   if (!e) return NK_OK;
+  mark_edges(v);
   return launch(K_EDGE, 8.0 * edge_n_ * 2,
                 [&] { return edge_gather_launch(v, e, edge_ny_, edge_nx_, s); });
 }

@@ -42,6 +42,7 @@ enum Kind : int {
   K_EDGE,
   K_ARN_SLAB,
   K_CTL,
+  K_PUSH,  // pushed halo rows of a producer (peer-memory slabs)
   K_NKINDS
 };
 
@@ -82,6 +83,15 @@ class Engine {
   }
   // The edge array of pool vector v (nullptr when v is not a pool vector or edges are off).
   double* edges(const double* v) const;
+  // index of pool vector v in the workspace pool (-1: not a pool vector); vectors in the pool
+  int64_t pool_index(const double* v) const;
+  int pool_count() const { return pool_count_; }
+  // v's edge array is maintained: every kernel that writes v also writes its edge array (the
+  // stencil passes' outputs, the fused kernel's, vectors refreshed by gather_edges); only those
+  // may be read in place of a stencil field's side columns.  (The LGMRES augmentation vectors
+  // are written by combinations only and are never marked.)
+  void mark_edges(const double* v);
+  bool edges_kept(const double* v) const;
   // Refresh the edge array of pool vector v from v (no-op without one).
   int gather_edges(const double* v);
   // Vector stride in the pool.  Large vectors get an odd multiple of 128 KiB: consecutive basis
@@ -154,6 +164,7 @@ class Engine {
   double* pool_ = nullptr;
   bool own_pool_ = false;
   int pool_count_ = 0;
+  std::vector<uint8_t> ekept_;  // per pool vector: mark_edges
   double* epool_ = nullptr;
   int64_t edge_ny_ = 0, edge_nx_ = 0, edge_n_ = 0;
   double* partial_ = nullptr;

@@ -94,6 +94,20 @@ __global__ void __launch_bounds__(kHaloBlock) peer_halo_kernel(const PeerArgs a,
   peer_halo_finish(a, nx, lo, hi);
 }
 
+// Pushed halo rows (arnoldi.hip): v's rows 0, 1 -> rows 2, 3 of the previous rank's slot, rows
+// ny-2, ny-1 -> rows 0, 1 of the next rank's slot, then a system-scope fence.  Nothing waits.
+__global__ void __launch_bounds__(kHaloBlock) push_rows_kernel(const double* v, double* pp,
+                                                              double* pn, int64_t ny, int64_t nx,
+                                                              int64_t ld) {
+  const int t = blockIdx.y;
+  const int64_t row = (t < 2) ? t : ny - 4 + t;
+  double* dst = (t < 2) ? pp + (2 + t) * ld : pn + (t - 2) * ld;
+  const int64_t step = int64_t(gridDim.x) * kHaloBlock;
+  for (int64_t j = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x; j < nx; j += step)
+    dst[j] = v[row * nx + j];
+  __threadfence_system();
+}
+
 // what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)
 struct PeerBlob {
   hipIpcMemHandle_t ipc;
@@ -137,6 +151,7 @@ struct PeerComm final : nk_comm {
   hipStream_t side = nullptr;  // abort writes (never queued behind a spinning collective)
   uint64_t red_tag = 0, halo_tag = 0;
   uint64_t ticks = 0;  // wait bound (wait_ticks)
+  const void* slot_owner = nullptr;  // the stepper holding the halo slots
   bool connected = false, same_dev = false, any_shared = false, aborted = false;
   PeerBlob blob{};
 
@@ -187,6 +202,21 @@ struct PeerComm final : nk_comm {
     *out = args(++red_tag);
     return true;
   }
+  bool claim_slots(const void* owner, nk_halo_slots* out) override {
+    if (!connected || !owner || (slot_owner && slot_owner != owner)) return false;
+    slot_owner = owner;
+    const int prev = (r - 1 + p) % p, next = (r + 1) % p;
+    const int64_t off = off_slots(p, max_nx);
+    out->mine = reinterpret_cast<double*>(base[r] + off);
+    out->prev = reinterpret_cast<double*>(base[prev] + off);
+    out->next = reinterpret_cast<double*>(base[next] + off);
+    out->ld = max_nx;
+    out->count = kHaloSlots;
+    return true;
+  }
+  void release_slots(const void* owner) override {
+    if (slot_owner == owner) slot_owner = nullptr;
+  }
   bool take_halo(PeerArgs* out, int64_t nx) override {
     if (!connected || failed() || nx > max_nx) return false;
     *out = args(++halo_tag);
@@ -230,6 +260,14 @@ struct PeerComm final : nk_comm {
 };
 
 }  // namespace
+
+hipError_t push_rows_launch(const double* v, double* prev_slot, double* next_slot, int64_t ny,
+                            int64_t nx, int64_t ld, hipStream_t s) {
+  if (!v || !prev_slot || !next_slot || ny < 4 || nx < 1 || nx > ld) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(push_rows_kernel, dim3(unsigned(halo_blocks(nx)), 4), dim3(kHaloBlock), 0, s,
+                     v, prev_slot, next_slot, ny, nx, ld);
+  return hipGetLastError();
+}
 
 bool peer_fuse_enabled() {
   const char* e = std::getenv("NKHIP_PEER_FUSE");

@@ -40,8 +40,14 @@ __host__ __device__ inline int64_t x_chunks(int64_t max_nx) { return (max_nx + k
 __host__ __device__ inline int64_t off_xflag(int P, int64_t max_nx) {
   return off_stage(P) + int64_t(2) * 2 * 2 * max_nx * 8;
 }
+// halo slots of the pushed-halo-rows path (arnoldi.hip "Pushed halo rows"): one per pool vector
+// of the stepper that claimed them, 4 rows of max_nx doubles each, after the chunk flags
+constexpr int64_t kHaloSlots = 2 * 64 + 8;  // >= the largest solver pool (vectors_needed)
+__host__ __device__ inline int64_t off_slots(int P, int64_t max_nx) {
+  return (off_xflag(P, max_nx) + int64_t(2) * 2 * x_chunks(max_nx) * 8 + 255) / 256 * 256;
+}
 __host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
-  return off_xflag(P, max_nx) + int64_t(2) * 2 * x_chunks(max_nx) * 8;
+  return off_slots(P, max_nx) + kHaloSlots * 4 * max_nx * 8;
 }
 
 struct PeerArgs {

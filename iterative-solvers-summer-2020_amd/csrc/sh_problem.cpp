@@ -62,6 +62,8 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
     }
     ny_min_ = int64_t(-mm[0]);
     ny_max_ = int64_t(mm[1]);
+    // the halo slots of the pushed-halo-rows path (peer-memory communicator, one stepper)
+    if (!E_.comm->claim_slots(this, &slots_) || slots_.ld < nx) slots_ = nk_halo_slots{};
     if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming) != hipSuccess) {
@@ -72,6 +74,7 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
 }
 
 SHProblem::~SHProblem() {
+  if (slots_.mine) E_.comm->release_slots(this);
   if (side_) hipStreamSynchronize(side_);
   if (B_) hipFree(B_);
   if (hx_) hipFree(hx_);
@@ -168,7 +171,31 @@ int SHProblem::prepare(const double* u_prev) {
 }
 
 int SHProblem::set_x0(const double* x0) { return halo(x0, hx_); }
-int SHProblem::set_dir(const double* d) { return halo(d, hd_); }
+int SHProblem::set_dir(const double* d) {
+  const int rc = halo(d, hd_);
+  return rc ? rc : push(d);  // d, the newest augmentation vector: z of later fused steps
+}
+
+bool SHProblem::push_mode() const {
+  if (!slots_.mine || E_.pool_count() > slots_.count || slab_x_enabled(E_.comm)) return false;
+  const char* e = std::getenv("NKHIP_SLAB_PUSH");
+  return !(e && e[0] == '0');
+}
+
+double* SHProblem::slot(double* base, const double* v) const {
+  const int64_t q = E_.pool_index(v);
+  return q < 0 ? nullptr : base + q * 4 * slots_.ld;
+}
+
+int SHProblem::push(const double* v) {
+  if (!push_mode() || !has_fused(1)) return NK_OK;
+  double* pp = slot(slots_.prev, v);
+  double* pn = slot(slots_.next, v);
+  if (!pp || !pn) return NK_OK;  // not a pool vector: never an entry of a fused step
+  return E_.launch(K_PUSH, 2.0 * 4 * 8 * nx_, [&] {
+    return push_rows_launch(v, pp, pn, ny_, nx_, slots_.ld, E_.s);
+  });
+}
 
 int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, double* F,
                     double* G, double red[3]) {
@@ -185,9 +212,11 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   A.c = c_;
   A.partial = E_.partial();
   set_edges(&A, F);
+  if (A.E0 && xt && (A.E2 = E_.edges(xt)) != nullptr) E_.mark_edges(xt);  // the next x0
   int64_t nblk = 0;
   int rc = E_.launch(K_TRIAL, stencil_bytes_per_point(SMode::TRIAL, xt != nullptr) * ny_ * nx_,
                      [&] { return stencil_launch(SMode::TRIAL, A, E_.s, &nblk); });
+  if (!rc) rc = push(F);  // F may become V_0 (before the all-reduce of the reduction below)
   if (rc) return rc;
   return E_.reduce(nblk, 1, 3, red);
 }
@@ -204,14 +233,17 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
     A.a = field(z, hz_);
     A.alpha = zs;
     A.p0 = x0;
-    return halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    return rc ? rc : push(w);
   }
   A.a = field(x0, hx_);
   A.b = field(z, hz_);
   A.alpha = sc * zs;
   A.p0 = G0;
   A.sc = sc;
-  return halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  side_edges(&A, x0, z);
+  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  return rc ? rc : push(w);
 }
 
 int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
@@ -227,12 +259,15 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
     A.a = field(z, hz_);
     A.p0 = x0;
-    return halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    return rc ? rc : push(w);
   }
   A.a = field(x0, hx_);
   A.b = field(z, hz_);
   A.p0 = G0;
-  return halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  side_edges(&A, x0, z);
+  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  return rc ? rc : push(w);
 }
 
 // One launch per Arnoldi step with the FD JVP (arnoldi.hip).  On a row slab the kernel needs u
@@ -281,6 +316,8 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     for (int i = 0; i <= nv; ++i) A.E[i] = nullptr;
   A.Eout_v = E_.edges(out_v);
   A.Eout_w = E_.edges(out_w);
+  if (A.Eout_v) E_.mark_edges(out_v);
+  if (A.Eout_w) E_.mark_edges(out_w);
   if (mb_) {
     const int mode = arnoldi_mbox_mode();
     if (mode != 0) {
@@ -305,6 +342,28 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   // interior pass loses more to the CUs it leaves for the exchange kernels, plus the two
   // latency-bound 2-row launches after it, than the exchange costs in series (0.678 vs 0.658 ms
   // per Arnoldi step); the default is one launch after the exchange.
+  // Pushed halo rows: every entry's halo rows already sit in this rank's slots (arnoldi.hip):
+  // one launch, no exchange before it; its outputs' edge rows go into the neighbours' slots
+  if (push_mode()) {
+    bool ok = true;
+    for (int i = 0; i < nv; ++i) ok = ok && (A.HS[i] = slot(slots_.mine, V[i])) != nullptr;
+    ok = ok && (A.HS[nv] = slot(slots_.mine, w)) != nullptr;
+    if (z) ok = ok && (A.HS[nv + 1] = slot(slots_.mine, z)) != nullptr;
+    ok = ok && (A.PS[0] = slot(slots_.prev, out_v)) != nullptr &&
+         (A.PS[1] = slot(slots_.next, out_v)) != nullptr &&
+         (A.PS[2] = slot(slots_.prev, out_w)) != nullptr &&
+         (A.PS[3] = slot(slots_.next, out_w)) != nullptr;
+    if (ok) {
+      A.hs_ld = slots_.ld;
+      A.yh = y4_;  // u on the halo rows, filled by the edge bands (4 rows of nx)
+      A.yh_ld = nx_;
+      last_split_ = false;
+      edge_launched_ = false;
+      return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+    }
+    for (int i = 0; i <= nv + 1; ++i) A.HS[i] = nullptr;
+    for (auto& p : A.PS) p = nullptr;
+  }
   const char* ov = std::getenv("NKHIP_SLAB_OVERLAP");
   const bool split = ny_ >= 12 && side_ && (ov && ov[0] == '1');
   last_split_ = split;
@@ -402,16 +461,29 @@ void SHProblem::void_fused_steps(int count) {
 
 // The edge array of a stencil pass's output, written by the pass itself (when the fused kernel
 // will read block halos from it): TRIAL's F becomes V_0, the JVP's w the next update entry.
-void SHProblem::set_edges(StencilArgs* A, const double* out) const {
+void SHProblem::set_edges(StencilArgs* A, const double* out) {
   if (!has_fused(1)) return;
   A->E0 = E_.edges(out);
   A->e_ny = ny_;
   A->e_row0 = 0;
+  if (A->E0) E_.mark_edges(out);
+}
+
+// The stencil fields' side columns from their edge arrays, where every writer of the field keeps
+// them (NKHIP_EDGES=0, read per call, reads the neighbouring blocks' lines instead)
+void SHProblem::side_edges(StencilArgs* A, const double* a, const double* b) const {
+  const char* e = std::getenv("NKHIP_EDGES");
+  if (!has_fused(1) || (e && e[0] == '0')) return;
+  A->e_ny = ny_;
+  A->e_row0 = 0;
+  if (a && E_.edges_kept(a)) A->Ea = E_.edges(a);
+  if (b && E_.edges_kept(b)) A->Eb = E_.edges(b);
 }
 
 int SHProblem::publish_edges(const double* v) {
   if (!has_fused(1)) return NK_OK;
-  return E_.gather_edges(v);
+  const int rc = E_.gather_edges(v);
+  return rc ? rc : push(v);
 }
 
 // ============================================================================================

@@ -31,7 +31,8 @@ class SHProblem final : public Problem {
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
   int publish_edges(const double* v) override;
-  void set_edges(StencilArgs* A, const double* out) const;
+  void set_edges(StencilArgs* A, const double* out);
+  void side_edges(StencilArgs* A, const double* a, const double* b) const;
   void void_fused_steps(int count) override;
 
  private:
@@ -41,6 +42,11 @@ class SHProblem final : public Problem {
   int halo(const double* v, double* h);
   // the JVP pass on a slab: halo of z + stencil; interior rows overlap the exchange
   int halo_stencil(int kind, SMode m, const StencilArgs& A, const double* z, double* zh);
+  // pushed halo rows (arnoldi.hip): on when the communicator lent this stepper its halo slots
+  // (NKHIP_SLAB_PUSH=0, read per call, turns it off)
+  bool push_mode() const;
+  double* slot(double* base, const double* v) const;  // v's halo slot in a slot region
+  int push(const double* v);  // v's edge rows into the neighbours' slots (push_rows_launch)
   Engine& E_;
   int64_t ny_, nx_, ny_g_;
   SHCoef c_;
@@ -61,6 +67,7 @@ class SHProblem final : public Problem {
   uint64_t mb_tag_ = 0;   // one tag per fused launch
   bool last_split_ = false;  // the last fused step ran as interior + edge-band launches
   bool edge_launched_ = false;  // the last fused step launched the slab edge kernel
+  nk_halo_slots slots_{};       // claimed from the communicator (mine == nullptr: none)
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):

@@ -192,19 +192,33 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
   double alpha, sc;
   jvp_scale<M>(A, &alpha, &sc);
 
-  auto ld = [&](const Field& f, int64_t r, double (&v)[6]) {
+  // the block's side columns (two each side) of an own row from the fields' edge arrays: the
+  // first thread's c-2, c-1 are boundary B0's slots 0, 1, the last thread's c+2, c+3 boundary
+  // B0 + 2 BX's slots 2, 3 (nk_kernels.h edge layout; 2 BX == kEdgeW)
+  static_assert(2 * BX == kEdgeW, "a march block is one edge group wide");
+  const int64_t nbE = edge_groups(nx);
+  const int64_t eL = (cc / kEdgeW) * A.e_ny * 4, eR = (((cc + 2) / kEdgeW) % nbE) * A.e_ny * 4 + 2;
+  const bool sideL = threadIdx.x == 0, sideR = threadIdx.x == BX - 1;
+  auto ld = [&](const Field& f, const double* E, int64_t r, double (&v)[6]) {
     const double* p = rowp_fast(f, r, ny, nx);
-    const double2 x0 = *reinterpret_cast<const double2*>(p + cm);
+    const double* pl = p + cm;
+    const double* pr = p + cp;
+    if (E && r >= 0 && r < ny) {  // own rows of this launch (halo rows come from lo / hi)
+      const int64_t er = (A.e_row0 + r) * 4;
+      pl = sideL ? E + eL + er : pl;
+      pr = sideR ? E + eR + er : pr;
+    }
+    const double2 x0 = *reinterpret_cast<const double2*>(pl);
     const double2 x1 = *reinterpret_cast<const double2*>(p + cc);
-    const double2 x2 = *reinterpret_cast<const double2*>(p + cp);
+    const double2 x2 = *reinterpret_cast<const double2*>(pr);
     v[0] = x0.x; v[1] = x0.y; v[2] = x1.x; v[3] = x1.y; v[4] = x2.x; v[5] = x2.y;
   };
   // ring[f][slot][6]: raw rows of field f (a, then b)
   double ring[NF][RING][6];
   auto load_row = [&](int slot, int64_t r) {
     r = (r > ny + 1) ? ny + 1 : ((r < -2) ? -2 : r);  // past the band: a valid halo / edge row
-    ld(A.a, r, ring[0][slot]);
-    if constexpr (NF == 2) ld(A.b, r, ring[1][slot]);
+    ld(A.a, A.Ea, r, ring[0][slot]);
+    if constexpr (NF == 2) ld(A.b, A.Eb, r, ring[1][slot]);
   };
   // a + alpha b, formed once when the row enters the window
   auto combine = [&](int slot) {
@@ -295,6 +309,16 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
         if constexpr (M == SMode::TRIAL) {
           *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
           if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+          if (A.E2) {  // out2's edge array, as out0's above
+            const int64_t er = A.e_row0 + r;
+            const double2 ev = make_double2(res[0].o2, res[1].o2);
+            if (cc % kEdgeW == 0)
+              *reinterpret_cast<double2*>(A.E2 + ((cc / kEdgeW) * A.e_ny + er) * 4 + 2) = ev;
+            if ((cc + 2) % kEdgeW == 0 || cc + 2 == nx) {
+              const int64_t b = (cc + 2 == nx) ? 0 : (cc + 2) / kEdgeW;
+              *reinterpret_cast<double2*>(A.E2 + (b * A.e_ny + er) * 4) = ev;
+            }
+          }
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             red[0] += res[q].o0 * res[q].o0;
@@ -430,7 +454,7 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     else
       hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY, int(gx), int(gy));
   } else {
-    if (A.E0) return hipErrorInvalidValue;  // edge arrays come with the march path only
+    if (A.E0 || A.E2 || A.Ea || A.Eb) return hipErrorInvalidValue;  // march path only
     const int64_t n = A.nx * A.ny;
     const int64_t g = (n + 255) / 256;
     if (nblk) *nblk = g;

@@ -206,6 +206,36 @@ comm.close()
 """
 
 
+def test_peer_world1_push_matches_exchange_bitwise(monkeypatch):
+    """The pushed-halo-rows path (default: every producer writes its edge rows into the
+    neighbours' halo slots, the fused kernel's edge bands form u on the halo rows from them) and
+    the edge + halo exchange kernel (NKHIP_SLAB_PUSH=0) give the same bits: the halo rows are the
+    same update sums in the same order."""
+    import nkhip
+    N = 128
+    U0 = np.random.default_rng(7).standard_normal((N, N))
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NKHIP_SLAB_PUSH", mode)
+        (comm,) = nkhip.peer_comms(1, N)
+        try:
+            m = nkhip.SwiftHohenberg(N=N, d=0.625 * N, f_tol=1e-10, comm=comm, ny_local=N,
+                                     profile=1)
+            U = torch.as_tensor(U0, device="cuda")
+            for _ in range(2):
+                U = m.step(U)
+            out[mode] = (U.cpu().numpy(), dict(m.last_stats), m.kernel_profile())
+            m.close()
+        finally:
+            comm.close()
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1]["nit"] == out["0"][1]["nit"]
+    # push mode: no slab edge kernel, the pushes instead; exchange mode: the edge kernel
+    assert out["1"][2].get("arnoldi_edge", {}).get("launches", 0) == 0
+    assert out["1"][2]["halo_push"]["launches"] > 0
+    assert out["0"][2]["arnoldi_edge"]["launches"] > 0
+
+
 @pytest.mark.timeout(200)
 def test_peer_abort_releases_blocked_rank(tmp_path):
     """nk_comm_abort's contract, across processes: rank 1 fails before its step and aborts;
