@@ -119,22 +119,16 @@ __device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, doub
   }
   const double gj = (lane < j) ? sig_j * sig * rg : 0.0;  // gram[j][lane]
   // Gram rows 0..j (k < row) in LDS for the column sweep (one wave: LDS keeps its order).  Every
-  // load is issued before the first LDS store (a fixed, unrolled count): one memory latency for
-  // the whole matrix instead of one per 64 entries.
+  // load is issued before the first LDS store (one row per unrolled iteration, no index
+  // division): one memory latency for the whole matrix instead of one per row.
   __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  {
-    constexpr int kG = ((kArnMaxNV + 1) * (kArnMaxNV + 1) + 63) / 64;
-    double gl[kG];
+  {  // lane k takes column k of rows k+1 .. j-1
+    double gl[kArnMaxNV];
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      const int q = lane + 64 * i, r = q / np, k = q % np;
-      gl[i] = (q < np * np && k < r && r < j) ? S->gram[r][k] : 0.0;
-    }
+    for (int r = 1; r < kArnMaxNV; ++r) gl[r] = (r < j && lane < r) ? S->gram[r][lane] : 0.0;
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      const int q = lane + 64 * i, r = q / np, k = q % np;
-      if (q < np * np && k < r && r < j) G[r][k] = gl[i];
-    }
+    for (int r = 1; r < kArnMaxNV; ++r)
+      if (r < j && lane < r) G[r][lane] = gl[r];
   }
   if (lane < j) G[j][lane] = gj;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

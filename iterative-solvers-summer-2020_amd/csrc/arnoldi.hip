@@ -357,58 +357,63 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
 // march as with exchanged halo rows.  No exchange runs between the control and this launch, and
 // no block waits for another rank.  (A halo column shared with the neighbouring block is written
 // by both with the same bits.)
-template <int NV, int KMAX>
+template <int NV>
 __device__ void slab_push_prologue(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW,
                                    int h0, const double* cst, double a_tau) {
   const int64_t nx = A.nx, ld = A.hs_ld;
   const bool first = band == 0, last = band == int64_t(A.nbands) - 1;
   double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
   constexpr int NE = NV + 1;
+  // (row, column) items per thread and round: each round's loads are in flight together (one
+  // memory latency); 2 x NE values stay below the march's register peak, so the prologue does
+  // not raise the kernel's register count (and with it lower its occupancy)
+  constexpr int KMAX = 2;
   const int64_t ncol = BW + 4;  // columns B0-2 .. B0+BW+1 of the two halo rows
-  const int64_t nb = blockDim.x;
+  const int64_t nb = blockDim.x, items = 2 * ncol;
   for (int side = 0; side < 2; ++side) {
     if (side == 0 ? !first : !last) continue;
-    // KMAX (row, column) items per thread (2 ncol <= KMAX blockDim for the layout), entry-major
-    // so that every item's loads are in flight together: one memory latency
-    int64_t off[KMAX], yo[KMAX];
-    bool on[KMAX];
+#pragma unroll 1
+    for (int64_t base = 0; base < items; base += KMAX * nb) {
+      int64_t off[KMAX], yo[KMAX];
+      bool on[KMAX];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int64_t i = threadIdx.x + k * nb;
-      on[k] = i < 2 * ncol;
-      const int64_t rr = (i >= ncol) ? 1 : 0;
-      const int64_t j = ((B0 - 2 + (i - rr * ncol)) % nx + nx) % nx;
-      const int64_t hrow = 2 * side + rr;  // slot / yh row: 0, 1 = rows -2, -1; 2, 3 = ny, ny+1
-      off[k] = on[k] ? CI(hrow * ld + j, 4 * ld) : 0;
-      yo[k] = on[k] ? CI(hrow * nx + j, 4 * nx) : 0;
-    }
-    double u[KMAX];
-    if (A.z) {
+      for (int k = 0; k < KMAX; ++k) {
+        const int64_t i = base + threadIdx.x + k * nb;
+        on[k] = i < items;
+        const int64_t rr = (i >= ncol) ? 1 : 0;
+        const int64_t j = ((B0 - 2 + (i - rr * ncol)) % nx + nx) % nx;
+        const int64_t hrow = 2 * side + rr;  // slot / yh row: 0, 1 = rows -2, -1; 2, 3 = ny, ny+1
+        off[k] = on[k] ? CI(hrow * ld + j, 4 * ld) : 0;
+        yo[k] = on[k] ? CI(hrow * nx + j, 4 * nx) : 0;
+      }
+      double u[KMAX];
+      if (A.z) {
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) u[k] = A.HS[NV + 1][off[k]];
-    } else {
-      double p0[KMAX], p1[KMAX];
+        for (int k = 0; k < KMAX; ++k) u[k] = A.HS[NV + 1][off[k]];
+      } else {
+        double x[KMAX][NE];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) p0[k] = p1[k] = 0.0;
+        for (int e = 0; e < NE; ++e)
 #pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const double cf = (e < NV) ? cst[e] : a_tau;
-        const bool even = (h0 > 0) ? (e < h0) : ((e & 1) == 0);
+          for (int k = 0; k < KMAX; ++k) x[k][e] = A.HS[e][off[k]];
 #pragma unroll
         for (int k = 0; k < KMAX; ++k) {
-          const double x = A.HS[e][off[k]];
-          if (even)
-            p0[k] = __builtin_fma(cf, x, p0[k]);
-          else
-            p1[k] = __builtin_fma(cf, x, p1[k]);
+          double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const double cf = (e < NV) ? cst[e] : a_tau;
+            if ((h0 > 0) ? (e < h0) : ((e & 1) == 0))
+              p0 = __builtin_fma(cf, x[k][e], p0);
+            else
+              p1 = __builtin_fma(cf, x[k][e], p1);
+          }
+          u[k] = p0 + p1;
         }
       }
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) u[k] = p0[k] + p1[k];
+      for (int k = 0; k < KMAX; ++k)
+        if (on[k]) yh[yo[k]] = u[k];
     }
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-      if (on[k]) yh[yo[k]] = u[k];
   }
   __threadfence_block();
   __syncthreads();
@@ -851,8 +856,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
 
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
-  // (2 (BW + 4) <= 3 blockDim: 128- and 256-column blocks of 2 and 4 waves)
-  if (edge_band) slab_push_prologue<NV, 3>(A, band, B0, BW, 0, cst, a_tau);  // uniform per block
+  if (edge_band) slab_push_prologue<NV>(A, band, B0, BW, 0, cst, a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
     // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
@@ -1276,8 +1280,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
 
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
-  // (2 (BW + 4) <= 5 blockDim: 512-column blocks of 4 waves)
-  if (edge_band) slab_push_prologue<NV, 5>(A, band, B0, BW, NV + 1, cst, a_tau);
+  if (edge_band) slab_push_prologue<NV>(A, band, B0, BW, NV + 1, cst, a_tau);
   if (nrows > 0) {
     Slot P[2];
     load(P[0], r0 - 2);

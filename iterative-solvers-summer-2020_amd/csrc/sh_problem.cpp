@@ -1,6 +1,7 @@
 // Swift-Hohenberg stepper problem and generic callback problem (see sh_problem.h).
 #include "sh_problem.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 

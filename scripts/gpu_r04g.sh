@@ -6,9 +6,9 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread \
-  > gpurun_out/r04f_tests.log 2>&1
+  > gpurun_out/r04g_tests.log 2>&1
 rc=$?
-tail -15 gpurun_out/r04f_tests.log
+tail -15 gpurun_out/r04g_tests.log
 [ $rc -eq 0 ] || exit $rc
 VARIANTS="plain peer peerex" bash scripts/ab_comm.sh 2 || exit 1
-bash scripts/ab_env.sh 2 "NKHIP_DEVCTL=0" "NKHIP_DEVCTL=1"
+bash scripts/ab_env.sh 1 "NKHIP_DEVCTL=0" "NKHIP_DEVCTL=1" "NKHIP_DEVCTL=0" "NKHIP_DEVCTL=1"

@@ -209,8 +209,8 @@ comm.close()
 def test_peer_world1_push_matches_exchange_bitwise(monkeypatch):
     """The pushed-halo-rows path (default: every producer writes its edge rows into the
     neighbours' halo slots, the fused kernel's edge bands form u on the halo rows from them) and
-    the edge + halo exchange kernel (NKHIP_SLAB_PUSH=0) give the same bits: the halo rows are the
-    same update sums in the same order."""
+    the edge + halo exchange kernel (NKHIP_SLAB_PUSH=0) give the same bits: the halo rows are
+    the same update sums in the same order."""
     import nkhip
     N = 128
     U0 = np.random.default_rng(7).standard_normal((N, N))
