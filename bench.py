@@ -157,7 +157,7 @@ def cpu_baseline(n, h, k, r, g, u_start, gpu_fevals_per_step):
     return rec, u_next
 
 
-def config2_lap5(n=1024, reps=200):
+def config2_lap5(n=1024, reps=200, rocprof=True):
     """Config 2: 1024^2 fp64 periodic 5-point Laplacian SpMV (sh_scipy_nk.py:32-35), 16 B/pt,
     timed with HIP events on torch's stream; the reference's CSR `Lap @ v` timed beside it."""
     import numpy as np
@@ -187,7 +187,11 @@ def config2_lap5(n=1024, reps=200):
         nkhip.lap5_apply(v, 1 / h ** 2, out=y)
         e1.record()
     torch.cuda.synchronize()
-    k_us = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e3 / reps
+    ev_us = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e3 / reps
+    # the kernel-only duration from a rocprofv3 trace of the same launches (an event pair around
+    # a ~5 us kernel measures mostly the events), else the event pairs
+    rp = config2_rocprof() if rocprof else None
+    k_us = rp["avg_us"] if rp else ev_us
     k_gbs = 16 * n * n / (k_us * 1e-6) / 1e9
     err = float(np.abs(y.cpu().numpy().reshape(-1) - sh_oracle.lap5(v_np, n, n, 1 / h ** 2)).max())
     L = sh_oracle.csr_lap(n, h)
@@ -202,12 +206,51 @@ def config2_lap5(n=1024, reps=200):
             "roofline": {"kernel": "march_kernel<LAP5>", "bound": "hbm",
                          "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4), "avg_us": round(k_us, 2),
-                         "alg_bytes_per_launch": 16 * n * n, "launches": reps,
+                         "alg_bytes_per_launch": 16 * n * n,
+                         "launches": rp["calls"] if rp else reps,
+                         "duration_source": ("rocprofv3 --kernel-trace --stats over "
+                                             "scripts/config2_kernel.py on this box" if rp else
+                                             "HIP event pair around each launch"),
+                         "event_pair_us": round(ev_us, 2),
                          "mall_resident": True,
-                         "note": "HIP event pair around each launch; the 16.8 MB working set "
-                                 "(v, y) stays in the 256 MB Infinity Cache between launches, "
-                                 "so HBM is not what bounds it"},
+                         "note": "the 16.8 MB working set (v, y) stays in the 256 MB Infinity "
+                                 "Cache between launches, so HBM is not what bounds it"},
             "note": "back-to-back launches; rocprofv3 durations in profiles/r02_config2.md"}
+
+
+def config2_rocprof():
+    """Config 2's kernel duration without launch gaps or event overhead: `rocprofv3
+    --kernel-trace --stats` over scripts/config2_kernel.py (205 back-to-back launches of the
+    1024^2 Laplacian, ~10 s), the average duration of march_kernel<LAP5>.  None without
+    rocprofv3 or when the pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    d = tempfile.mkdtemp(prefix="nkhip_c2_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        r = subprocess.run([prof, "--kernel-trace", "--stats", "-d", d, "-o", "c2",
+                            "--output-format", "csv", "--", sys.executable,
+                            os.path.join(ROOT, "scripts", "config2_kernel.py")],
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150,
+                           env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+        if r.returncode != 0:
+            return None
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("kernel_stats.csv"):
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        if "march_kernel" in row["Name"]:
+                            return {"avg_us": float(row["AverageNs"]) / 1e3,
+                                    "calls": int(row["Calls"])}
+        return None
+    except (OSError, ValueError, KeyError, subprocess.SubprocessError):
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def config3_droplet(steps=5, cpu_steps=2):
@@ -788,7 +831,8 @@ def main():
             del ua, ub, u_cpu
             out["cpu_baseline"] = rec
         if world == 1 and args.extra == "on":
-            out["other_configs"] = {"config2": config2_lap5(), "config3": config3_droplet(),
+            out["other_configs"] = {"config2": config2_lap5(rocprof=args.pmc == "auto"),
+                                    "config3": config3_droplet(),
                                     "config5_1gpu": config5_one_gpu(),
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),
                                     "droplet_init": config_droplet_init()}
