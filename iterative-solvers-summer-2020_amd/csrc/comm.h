@@ -73,6 +73,10 @@ struct nk_comm {
   // The halo slots, for one stepper at a time (`owner`); false: none (not the peer-memory
   // communicator, or another stepper holds them).  release_slots hands them back.
   virtual bool claim_slots(const void* /*owner*/, nk_halo_slots* /*out*/) { return false; }
+  // All-reduces this rank has issued so far (every rank counts the same sequence): a write into
+  // the neighbours' halo slots issued before all-reduce e is visible to every rank's launches
+  // issued after it, i.e. once epoch() > e.
+  virtual uint64_t epoch() const { return 0; }
   virtual void release_slots(const void* /*owner*/) {}
 };
 

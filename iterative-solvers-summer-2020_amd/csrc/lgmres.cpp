@@ -313,9 +313,10 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
       return combo_launch(w, w, tau, U, j + 1, n, E_.partial(), E_.s, &nblk);
     });
+    // v_{j+1}'s edge array (and pushed edge rows), before the all-reduce below orders them
+    if (!rc) rc = P_.publish_edges(w);
     // only |v_{j+1}|^2 is used (a non-finite v shows up in it): one sum, one all-reduce on N GPUs
     if (!rc) rc = E_.reduce_async(nblk, 1, 1, Engine::kSlotCombo);
-    if (!rc) rc = P_.publish_edges(w);
     if (rc) return rc;
     // speculatively start step j+1 with its scale taken from the device norm
     const bool spec = next_is_v && P_.has_dev_scale() && P_.may_speculate();
@@ -367,6 +368,9 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   rc = E_.launch(K_COMBO, 8.0 * n * (j + 2), [&] {
     return combo_launch(d, nullptr, 0.0, Z, j + 1, n, E_.partial(), E_.s, &nblk);
   });
+  // d: the line search's direction and the newest augmentation vector (z of later fused steps):
+  // its edge array, and on pushed-halo slabs its edge rows, before the all-reduce below
+  if (!rc) rc = P_.publish_edges(d);
   if (rc) return rc;
   double r2[2];
   rc = E_.reduce(nblk, 1, 2, r2);

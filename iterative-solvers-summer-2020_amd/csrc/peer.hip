@@ -214,6 +214,7 @@ struct PeerComm final : nk_comm {
     out->count = kHaloSlots;
     return true;
   }
+  uint64_t epoch() const override { return red_tag; }
   void release_slots(const void* owner) override {
     if (slot_owner == owner) slot_owner = nullptr;
   }

@@ -114,6 +114,8 @@ StencilArgs sub_args(const StencilArgs& A, int64_t r0, int64_t r1) {
 
 int SHProblem::halo_stencil(int kind, SMode m, const StencilArgs& A, const double* z, double* zh) {
   const double bytes = stencil_bytes_per_point(m, false);
+  if (!z)  // the halo rows are already in place (pushed slots): just the pass
+    return E_.launch(kind, bytes * ny_ * nx_, [&] { return stencil_launch(m, A, E_.s, nullptr); });
   if (!dist() || ny_ < 8 || !side_) {
     int rc = halo(z, zh);
     if (rc) return rc;
@@ -171,10 +173,36 @@ int SHProblem::prepare(const double* u_prev) {
                    [&] { return stencil_launch(SMode::BOLD, A, E_.s, nullptr); });
 }
 
-int SHProblem::set_x0(const double* x0) { return halo(x0, hx_); }
+// The halo of the Newton iterate / the search direction: from the pushed slots when the producer
+// pushed them before an all-reduce issued since (the TRIAL pass pushes x + alpha p, the final
+// combination pushes d), else exchanged
+int SHProblem::set_x0(const double* x0) {
+  hxp_ = slot_halo(x0);
+  if (hxp_) return NK_OK;
+  hxp_ = hx_;
+  return halo(x0, hx_);
+}
 int SHProblem::set_dir(const double* d) {
-  const int rc = halo(d, hd_);
-  return rc ? rc : push(d);  // d, the newest augmentation vector: z of later fused steps
+  hdp_ = slot_halo(d);
+  if (hdp_) return NK_OK;
+  hdp_ = hd_;
+  return halo(d, hd_);
+}
+
+void SHProblem::pushed(const double* v) {
+  const int64_t q = E_.pool_index(v);
+  if (q < 0) return;
+  if (push_ep_.size() < size_t(E_.pool_count())) push_ep_.assign(E_.pool_count(), ~uint64_t(0));
+  push_ep_[q] = E_.comm->epoch();
+}
+
+const double* SHProblem::slot_halo(const double* v) const {
+  if (!push_mode() || slots_.ld != nx_ || !has_fused(1)) return nullptr;
+  const int64_t q = E_.pool_index(v);
+  if (q < 0 || size_t(q) >= push_ep_.size() || push_ep_[q] == ~uint64_t(0) ||
+      !(E_.comm->epoch() > push_ep_[q]))
+    return nullptr;
+  return slots_.mine + q * 4 * slots_.ld;
 }
 
 bool SHProblem::push_mode() const {
@@ -193,9 +221,11 @@ int SHProblem::push(const double* v) {
   double* pp = slot(slots_.prev, v);
   double* pn = slot(slots_.next, v);
   if (!pp || !pn) return NK_OK;  // not a pool vector: never an entry of a fused step
-  return E_.launch(K_PUSH, 2.0 * 4 * 8 * nx_, [&] {
+  const int rc = E_.launch(K_PUSH, 2.0 * 4 * 8 * nx_, [&] {
     return push_rows_launch(v, pp, pn, ny_, nx_, slots_.ld, E_.s);
   });
+  if (!rc) pushed(v);
+  return rc;
 }
 
 int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, double* F,
@@ -203,8 +233,8 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   StencilArgs A;
   A.ny = ny_;
   A.nx = nx_;
-  A.a = field(x, hx_);
-  A.b = (p == x) ? field(x, hx_) : field(p, hd_);
+  A.a = field(x, hxp_ ? hxp_ : hx_);
+  A.b = (p == x) ? A.a : field(p, hdp_ ? hdp_ : hd_);
   A.alpha = alpha;
   A.p0 = B_;
   A.out0 = F;
@@ -218,6 +248,7 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   int rc = E_.launch(K_TRIAL, stencil_bytes_per_point(SMode::TRIAL, xt != nullptr) * ny_ * nx_,
                      [&] { return stencil_launch(SMode::TRIAL, A, E_.s, &nblk); });
   if (!rc) rc = push(F);  // F may become V_0 (before the all-reduce of the reduction below)
+  if (!rc && xt) rc = push(xt);  // ... and xt the next iterate x0
   if (rc) return rc;
   return E_.reduce(nblk, 1, 3, red);
 }
@@ -230,20 +261,21 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
   A.c = c_;
   A.out0 = w;
   set_edges(&A, w);
+  const double* zsh = slot_halo(z);  // z's halo rows already here (pushed): no exchange
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
-    A.a = field(z, hz_);
+    A.a = field(z, zsh ? zsh : hz_);
     A.alpha = zs;
     A.p0 = x0;
-    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, zsh ? nullptr : z, hz_);
     return rc ? rc : push(w);
   }
-  A.a = field(x0, hx_);
-  A.b = field(z, hz_);
+  A.a = field(x0, hxp_ ? hxp_ : hx_);
+  A.b = field(z, zsh ? zsh : hz_);
   A.alpha = sc * zs;
   A.p0 = G0;
   A.sc = sc;
   side_edges(&A, x0, z);
-  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, zsh ? nullptr : z, hz_);
   return rc ? rc : push(w);
 }
 
@@ -257,17 +289,18 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   set_edges(&A, w);
   A.znorm2 = znorm2;
   A.omega = omega;
+  const double* zsh = slot_halo(z);
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
-    A.a = field(z, hz_);
+    A.a = field(z, zsh ? zsh : hz_);
     A.p0 = x0;
-    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, z, hz_);
+    const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, zsh ? nullptr : z, hz_);
     return rc ? rc : push(w);
   }
-  A.a = field(x0, hx_);
-  A.b = field(z, hz_);
+  A.a = field(x0, hxp_ ? hxp_ : hx_);
+  A.b = field(z, zsh ? zsh : hz_);
   A.p0 = G0;
   side_edges(&A, x0, z);
-  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, z, hz_);
+  const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, zsh ? nullptr : z, hz_);
   return rc ? rc : push(w);
 }
 
@@ -356,6 +389,8 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
          (A.PS[3] = slot(slots_.next, out_w)) != nullptr;
     if (ok) {
       A.hs_ld = slots_.ld;
+      pushed(out_v);
+      pushed(out_w);
       A.yh = y4_;  // u on the halo rows, filled by the edge bands (4 rows of nx)
       A.yh_ld = nx_;
       last_split_ = false;

@@ -47,6 +47,10 @@ class SHProblem final : public Problem {
   bool push_mode() const;
   double* slot(double* base, const double* v) const;  // v's halo slot in a slot region
   int push(const double* v);  // v's edge rows into the neighbours' slots (push_rows_launch)
+  void pushed(const double* v);  // v's rows went out now (records the all-reduce epoch)
+  // v's halo rows as a stencil field's halo (4 rows: lo, hi) straight from this rank's slot, when
+  // the rows were pushed before an all-reduce already issued; nullptr: exchange them
+  const double* slot_halo(const double* v) const;
   Engine& E_;
   int64_t ny_, nx_, ny_g_;
   SHCoef c_;
@@ -68,6 +72,9 @@ class SHProblem final : public Problem {
   bool last_split_ = false;  // the last fused step ran as interior + edge-band launches
   bool edge_launched_ = false;  // the last fused step launched the slab edge kernel
   nk_halo_slots slots_{};       // claimed from the communicator (mine == nullptr: none)
+  std::vector<uint64_t> push_ep_;  // per pool vector: comm epoch of its last push (~0: none)
+  const double* hxp_ = nullptr;  // the halo of the current x0 / direction (hx_ / hd_ or a slot)
+  const double* hdp_ = nullptr;
 };
 
 // newton_krylov(F, xin) for an arbitrary device residual (droplet.py:383, PMA2_nk.py:100, ...):
