@@ -79,6 +79,12 @@ struct StencilArgs {
   const double* Ea = nullptr;
   const double* Eb = nullptr;
   int64_t e_ny = 0, e_row0 = 0;
+  // pushed halo rows (peer-memory slabs, arnoldi.hip): out0's / out2's rows 0, 1 and e_ny-2,
+  // e_ny-1 also go into the previous / next rank's halo slot ([0] / [1], row stride ps_ld), with
+  // a system-scope fence -- what push_rows_launch would do after the pass
+  double* PS0[2] = {};
+  double* PS2[2] = {};
+  int64_t ps_ld = 0;
   bool rev = false;    // set by stencil_launch (traversal_reverse)
   bool nt_p0 = false;  // set by stencil_launch: non-temporal loads of the point-wise input
 };

@@ -189,6 +189,28 @@ int SHProblem::set_dir(const double* d) {
   return halo(d, hd_);
 }
 
+// A stencil pass's outputs pushed in-kernel (pushed halo rows): out0 (and out2) into the
+// neighbours' slots, with the pass (march path: A->E0 set, so e_ny / e_row0 are)
+void SHProblem::set_push(StencilArgs* A, const double* out0, const double* out2) {
+  if (!push_mode() || !A->E0) return;
+  double* p0 = slot(slots_.prev, out0);
+  double* n0 = slot(slots_.next, out0);
+  if (!p0 || !n0) return;
+  A->PS0[0] = p0;
+  A->PS0[1] = n0;
+  A->ps_ld = slots_.ld;
+  pushed(out0);
+  if (out2) {
+    double* p2 = slot(slots_.prev, out2);
+    double* n2 = slot(slots_.next, out2);
+    if (p2 && n2) {
+      A->PS2[0] = p2;
+      A->PS2[1] = n2;
+      pushed(out2);
+    }
+  }
+}
+
 void SHProblem::pushed(const double* v) {
   const int64_t q = E_.pool_index(v);
   if (q < 0) return;
@@ -244,11 +266,12 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   A.partial = E_.partial();
   set_edges(&A, F);
   if (A.E0 && xt && (A.E2 = E_.edges(xt)) != nullptr) E_.mark_edges(xt);  // the next x0
+  set_push(&A, F, xt);
   int64_t nblk = 0;
   int rc = E_.launch(K_TRIAL, stencil_bytes_per_point(SMode::TRIAL, xt != nullptr) * ny_ * nx_,
                      [&] { return stencil_launch(SMode::TRIAL, A, E_.s, &nblk); });
-  if (!rc) rc = push(F);  // F may become V_0 (before the all-reduce of the reduction below)
-  if (!rc && xt) rc = push(xt);  // ... and xt the next iterate x0
+  // (F may become V_0 and xt the next iterate x0: their edge rows went into the neighbours'
+  // slots in the pass, before the all-reduce of the reduction below)
   if (rc) return rc;
   return E_.reduce(nblk, 1, 3, red);
 }
@@ -261,13 +284,14 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
   A.c = c_;
   A.out0 = w;
   set_edges(&A, w);
+  set_push(&A, w, nullptr);
   const double* zsh = slot_halo(z);  // z's halo rows already here (pushed): no exchange
   if (jvp_mode_ == NK_JVP_ANALYTIC) {
     A.a = field(z, zsh ? zsh : hz_);
     A.alpha = zs;
     A.p0 = x0;
     const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, zsh ? nullptr : z, hz_);
-    return rc ? rc : push(w);
+    return rc;
   }
   A.a = field(x0, hxp_ ? hxp_ : hx_);
   A.b = field(z, zsh ? zsh : hz_);
@@ -276,7 +300,7 @@ int SHProblem::jvp(const double* x0, const double* G0, const double* z, double z
   A.sc = sc;
   side_edges(&A, x0, z);
   const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, zsh ? nullptr : z, hz_);
-  return rc ? rc : push(w);
+  return rc;
 }
 
 int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
@@ -287,6 +311,7 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
   A.c = c_;
   A.out0 = w;
   set_edges(&A, w);
+  set_push(&A, w, nullptr);
   A.znorm2 = znorm2;
   A.omega = omega;
   const double* zsh = slot_halo(z);
@@ -294,14 +319,14 @@ int SHProblem::jvp_dev(const double* x0, const double* G0, const double* z, cons
     A.a = field(z, zsh ? zsh : hz_);
     A.p0 = x0;
     const int rc = halo_stencil(K_AJVP, SMode::AJVP, A, zsh ? nullptr : z, hz_);
-    return rc ? rc : push(w);
+    return rc;
   }
   A.a = field(x0, hxp_ ? hxp_ : hx_);
   A.b = field(z, zsh ? zsh : hz_);
   A.p0 = G0;
   side_edges(&A, x0, z);
   const int rc = halo_stencil(K_FDJVP, SMode::FDJVP, A, zsh ? nullptr : z, hz_);
-  return rc ? rc : push(w);
+  return rc;
 }
 
 // One launch per Arnoldi step with the FD JVP (arnoldi.hip).  On a row slab the kernel needs u

@@ -48,6 +48,7 @@ class SHProblem final : public Problem {
   double* slot(double* base, const double* v) const;  // v's halo slot in a slot region
   int push(const double* v);  // v's edge rows into the neighbours' slots (push_rows_launch)
   void pushed(const double* v);  // v's rows went out now (records the all-reduce epoch)
+  void set_push(StencilArgs* A, const double* out0, const double* out2);
   // v's halo rows as a stencil field's halo (4 rows: lo, hi) straight from this rank's slot, when
   // the rows were pushed before an all-reduce already issued; nullptr: exchange them
   const double* slot_halo(const double* v) const;

@@ -259,6 +259,15 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
   for (int k = 0; k < NR - 1; ++k) combine(k);
 
   double red[3] = {0.0, 0.0, 0.0};
+  bool pushed = false;  // this thread wrote rows into a neighbour's halo slot (fence at the end)
+  // a pushed edge row (global slab row g of e_ny) of an output into the neighbours' slots
+  auto push_row = [&](double* const* ps, int64_t g, double2 v) {
+    const bool top = g < 2, bot = g >= A.e_ny - 2;
+    if (!(top || bot)) return;
+    double* d = top ? ps[0] + (2 + g) * A.ps_ld : ps[1] + (g - (A.e_ny - 2)) * A.ps_ld;
+    *reinterpret_cast<double2*>(d + cc) = v;
+    pushed = true;
+  };
   for (int64_t base = 0; base < nrows; base += RING) {
 #pragma unroll
     for (int u = 0; u < RING; ++u) {
@@ -296,6 +305,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
       if (active && it < nrows) {
         const int64_t o = r * nx + cc;
         *reinterpret_cast<double2*>(A.out0 + o) = make_double2(res[0].o0, res[1].o0);
+        if (A.PS0[0]) push_row(A.PS0, A.e_row0 + r, make_double2(res[0].o0, res[1].o0));
         if (A.E0) {  // the edge array: E[(b e_ny + row) 4 + 0..3] = columns B-2, B-1, B, B+1
           const int64_t er = A.e_row0 + r;
           const double2 ev = make_double2(res[0].o0, res[1].o0);
@@ -309,6 +319,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
         if constexpr (M == SMode::TRIAL) {
           *reinterpret_cast<double2*>(A.out1 + o) = make_double2(res[0].o1, res[1].o1);
           if (A.out2) *reinterpret_cast<double2*>(A.out2 + o) = make_double2(res[0].o2, res[1].o2);
+          if (A.PS2[0]) push_row(A.PS2, A.e_row0 + r, make_double2(res[0].o2, res[1].o2));
           if (A.E2) {  // out2's edge array, as out0's above
             const int64_t er = A.e_row0 + r;
             const double2 ev = make_double2(res[0].o2, res[1].o2);
@@ -333,6 +344,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
       }
     }
   }
+  if (pushed) __threadfence_system();  // the pushed rows, before the pass ends
   if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
     const int64_t nblk = int64_t(gx) * gy;
@@ -454,7 +466,8 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
     else
       hipLaunchKernelGGL((march_kernel<M, BX, 1>), grid, dim3(BX), 0, s, B, RY, int(gx), int(gy));
   } else {
-    if (A.E0 || A.E2 || A.Ea || A.Eb) return hipErrorInvalidValue;  // march path only
+    if (A.E0 || A.E2 || A.Ea || A.Eb || A.PS0[0] || A.PS2[0])
+      return hipErrorInvalidValue;  // march path only
     const int64_t n = A.nx * A.ny;
     const int64_t g = (n + 255) / 256;
     if (nblk) *nblk = g;
