@@ -109,6 +109,46 @@ def pmc_traffic(args):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def trace_durations(args):
+    """Kernel-only durations on THIS box: `rocprofv3 --kernel-trace --stats` over a child run of
+    this bench (1 warmup + 1 step, same grid).  An event pair around a launch that starts on an
+    idle queue (the first JVP of every LGMRES call follows the host's line-search round trip)
+    also times the dispatch of the launch; the trace does not.  {kernel name: (calls, avg_us)},
+    or None without rocprofv3 or when the pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    d = tempfile.mkdtemp(prefix="nkhip_kt_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1",
+             "--n", str(args.n), "--jvp", args.jvp, "--extra", "off", "--cpu-baseline", "off",
+             "--pmc", "off", "--probes", "off"]
+    try:
+        r = subprocess.run([prof, "--kernel-trace", "--stats", "-d", d, "-o", "kt",
+                            "--output-format", "csv", "--"] + child,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150,
+                           env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+        if r.returncode != 0:
+            return None
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("kernel_stats.csv"):
+                    return {row["Name"]: (int(row["Calls"]), float(row["AverageNs"]) / 1e3)
+                            for row in csv.DictReader(open(os.path.join(root, f)))}
+        return None
+    except (OSError, ValueError, KeyError, subprocess.SubprocessError):
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+# the trace name of a kernel class the solver's launch log names (stencil modes: nk::SMode)
+TRACE_NAMES = {"sh_fdjvp": "march_kernel<(nk::SMode)5,", "sh_ajvp": "march_kernel<(nk::SMode)6,"}
+
+
 def cpu_baseline(n, h, k, r, g, u_start, gpu_fevals_per_step):
     """The reference's CPU path (scipy CSR L + scipy.optimize.newton_krylov on the reference
     residual, oracle/sh_oracle.py) timed on ONE full implicit step at the full grid size, from
@@ -731,6 +771,7 @@ def main():
         # PMC traffic of this run (two child passes under rocprofv3), else the last profile's
         live = pmc_traffic(args) if (world == 1 and args.pmc == "auto") else None
         traffic_db = live or load_traffic()
+        trace = trace_durations(args) if (world == 1 and args.pmc == "auto") else None
 
         def roof(name):
             v = ker[name]
@@ -795,6 +836,19 @@ def main():
             "final_step_check": final_check,
             "cpu_baseline": None,
         }
+        jr = out["jvp_roofline"]
+        hits = [cu for nm, cu in (trace or {}).items() if TRACE_NAMES.get(jvp_name, "\0") in nm]
+        if jr and hits:
+            # the JVP's kernel duration from the trace (its event pairs start on an idle queue)
+            calls = sum(c for c, _ in hits)
+            us = sum(c * u for c, u in hits) / calls
+            gbs = jr["alg_bytes_per_launch"] / (us * 1e-6) / 1e9
+            jr.update({"event_avg_us": jr["avg_us"], "event_frac": jr["frac"],
+                       "avg_us": round(us, 2), "achieved": round(gbs, 1),
+                       "frac": round(gbs / HBM_PEAK_GBS, 4), "trace_launches": calls,
+                       "duration_source": "rocprofv3 --kernel-trace --stats over a child run of "
+                                          "this bench (1 warmup + 1 step, same grid, this box); "
+                                          "event_avg_us: HIP event pairs in the timed run"})
         if slab_ab is not None:
             out["slab_exchange_ab"] = slab_ab
         if one_device:

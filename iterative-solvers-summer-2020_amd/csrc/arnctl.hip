@@ -14,175 +14,13 @@
 
 #include "nk_device.h"
 #include "nk_kernels.h"
+#include "arnctl_dev.h"
 #include "peer_dev.h"
 
 namespace nk {
 namespace {
 
-static_assert(kArnMaxNV + 1 <= 64, "one lane per basis entry");
 constexpr int RB = 1024;  // reduction block (as reduce_final_kernel)
-
-__device__ __forceinline__ double bcast(double v, int l) {  // lane l's v, l wave-uniform
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(b), l);
-  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(b >> 32), l);
-  return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-}
-
-// The control of step t, run by the first wave of a block (the other waves of the block must not
-// take part).  S: device state, H: the host's pinned copy (committed values go to both).
-__device__ void ctl_body(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
-                         double* prm, uint32_t* status, int t) {
-  const int lane = threadIdx.x & 63;
-  // the same field of H as p of S
-  auto mirror = [&](auto* p) {
-    return reinterpret_cast<decltype(p)>(reinterpret_cast<char*>(H) +
-                                         (reinterpret_cast<char*>(p) - reinterpret_cast<char*>(S)));
-  };
-  auto put = [&](auto* p, auto v) {
-    *p = v;
-    *mirror(p) = v;
-  };
-  // every load up front (one latency, not a chain): the step is t, and anything that says
-  // otherwise hands it back
-  const int j = t;
-  const int np = j + 1;
-  const int32_t halted = S->halt, sj = S->j, pending = S->hn_pending, nvm = S->nv_max, m = S->m;
-  const bool on = lane <= j;
-  const double rv = on ? red[lane] : 0.0;       // w_j . V_i
-  const double rg = on ? red[np + lane] : 0.0;  // V_j . V_i (lane j: |V_j|^2)
-  const double ww_raw = red[2 * np];            // |w_j|^2
-  double sig = (lane <= j) ? S->sig[lane] : 0.0;
-  const double hprev = (lane < j) ? S->h[lane] : 0.0;  // MGS coefficients of step j - 1
-  const double csl = (lane < j) ? S->cs[lane] : 0.0;
-  const double snl = (lane < j) ? S->sn[lane] : 0.0;
-  const double wn_i = S->wnorm[j > 0 ? j - 1 : 0], gvi = S->gv[j > 0 ? j - 1 : 0];
-  const double se = S->sig_est[j], ptol = S->ptol, omega = S->omega, lr2 = S->lag_ratio2;
-  const int32_t steps = S->steps;
-  if (halted) return;  // an earlier step was handed back: the host takes over from there
-  if (red_host) {  // the results of step t for the host (read if this step is handed back)
-    for (int i = lane; i <= 2 * np; i += 64) red_host[i] = red[i];
-  }
-  // hand step j back to the host unchanged (the host loop redoes it from the same state)
-  auto hand_back = [&] {
-    if (lane == 0) {
-      put(&S->halt, int32_t(1 + j));
-      prm[kArnMaxNV + 3] = 1.0;  // the fused step queued behind this control does nothing
-    }
-    __threadfence_system();
-    if (lane == 0) __hip_atomic_store(status + t, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  };
-  if (sj != t || !pending || j < 1 || j + 1 > nvm || j + 1 >= m) {
-    hand_back();
-    return;
-  }
-
-  // -- finish step i = j - 1 with hn = |V_j| (lgmres.cpp `finish`)
-  const int i = j - 1;
-  const double hn = std::sqrt(bcast(rg, j));
-  const double alpha = 1.0 / hn;
-  const double sig_j = std::isfinite(alpha) ? alpha : 1.0;
-  const bool breakdown = !(hn > DBL_EPSILON * wn_i);
-  // Givens sweep over hcur[0..i+1] = (h_0 .. h_i, hn): hcur[k] settles at sweep k
-  double a = bcast(hprev, 0);
-  double rcol = 0.0;  // lane k: R[k][i]
-  for (int k = 0; k < i; ++k) {
-    const double b = bcast(hprev, k + 1);
-    const double c = bcast(csl, k), s = bcast(snl, k);
-    const double tk = c * a + s * b;
-    a = -s * a + c * b;
-    if (lane == k) rcol = tk;
-  }
-  // givens(hcur[i], hn) (nk_solver.cpp detail::givens)
-  double ci = 1.0, si = 0.0;
-  if (hn != 0.0) {
-    const double r = std::hypot(a, hn);
-    ci = a / r;
-    si = hn / r;
-  }
-  const double rii = ci * a + si * hn;
-  if (lane == i) rcol = rii;
-  const double gv_next = -si * gvi, gv_i = ci * gvi;
-  if (std::fabs(gv_next) < ptol || breakdown) {
-    hand_back();
-    return;
-  }
-  double tau = 1.0;
-  if (se > 0.0) tau = sig_j / se;  // JVP_j saw V_j scaled by the estimate, not sig_j
-  if (lane == j) sig = sig_j;
-
-  // -- step j: |w|, Gram row, MGS coefficients (I + L) h = V^T w
-  const double ww = tau * tau * ww_raw;
-  if (!std::isfinite(ww)) {
-    hand_back();
-    return;
-  }
-  const double gj = (lane < j) ? sig_j * sig * rg : 0.0;  // gram[j][lane]
-  // Gram rows 0..j (k < row) in LDS for the column sweep (one wave: LDS keeps its order).  Every
-  // load is issued before the first LDS store (one row per unrolled iteration, no index
-  // division): one memory latency for the whole matrix instead of one per row.
-  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  {  // lane k takes column k of rows k+1 .. j-1
-    double gl[kArnMaxNV];
-#pragma unroll
-    for (int r = 1; r < kArnMaxNV; ++r) gl[r] = (r < j && lane < r) ? S->gram[r][lane] : 0.0;
-#pragma unroll
-    for (int r = 1; r < kArnMaxNV; ++r)
-      if (r < j && lane < r) G[r][lane] = gl[r];
-  }
-  if (lane < j) G[j][lane] = gj;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double acc = on ? tau * sig * rv : 0.0;
-  double hh = 0.0;
-  for (int k = 0; k <= j; ++k) {
-    const double hk = bcast(acc, k);  // final: every k' < k has been subtracted
-    hh += hk * hk;
-    if (lane > k && on) acc -= G[lane][k] * hk;
-  }
-  const double est = ww - hh;  // |v_{j+1}|^2 = |w|^2 - |h|^2
-  if (!(est > lr2 * ww)) {
-    hand_back();
-    return;
-  }
-  const double e = std::sqrt(est);
-  const double zs = 1.0 / e;
-  const double zn = zs * e;
-  if (zn == 0.0) {
-    hand_back();
-    return;
-  }
-  const double sc = omega / zn;
-
-  // -- commit step i's Hessenberg column and step j, then the fused step's parameters
-  if (lane <= i) put(&S->R[lane][i], rcol);
-  if (lane < j) put(&S->gram[j][lane], gj);
-  if (on) put(&S->h[lane], acc);
-  if (lane < kArnMaxNV) prm[lane] = on ? -acc * sig : 0.0;
-  if (lane == 0) {
-    put(&S->cs[i], ci);
-    put(&S->sn[i], si);
-    put(&S->gv[i], gv_i);
-    put(&S->gv[i + 1], gv_next);
-    put(&S->sig[j], sig_j);
-    put(&S->rn[j], hn);
-    if (se > 0.0) put(&S->zs[j], sig_j);
-    put(&S->wnorm[j], std::sqrt(ww));
-    put(&S->sig_est[j + 1], zs);
-    put(&S->zs[j + 1], zs);
-    put(&S->j, int32_t(j + 1));
-    put(&S->hn_pending, int32_t(1));
-    put(&S->steps, steps + 1);
-    prm[kArnMaxNV] = tau;
-    prm[kArnMaxNV + 1] = sc * zs;
-    prm[kArnMaxNV + 2] = sc;
-    prm[kArnMaxNV + 3] = 0.0;
-  }
-  // no fence: the host reads nothing on a continued step (it reads the mirror after a hand-back,
-  // whose release fence follows these writes in stream order)
-  if (lane == 0) __hip_atomic_store(status + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // up > 0: first copy the host's pinned loop state H to S (the fields before R, and the Gram rows
 // 0 .. up-2) -- the entry of a run of device steps, which would otherwise take two runtime blits
@@ -209,8 +47,9 @@ __device__ void upload_state(ArnCtlState* S, const ArnCtlState* H, int rows) {
 __global__ void __launch_bounds__(64) arn_ctl_kernel(ArnCtlState* S, ArnCtlState* H,
                                                      const double* red, double* red_host,
                                                      double* prm, uint32_t* status, int t, int up) {
+  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
   if (up > 0) upload_state(S, H, up - 1);
-  ctl_body(S, H, red, red_host, prm, status, t);
+  ctl_body(S, H, red, red_host, prm, status, t, G);
 }
 
 __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partial, int64_t nblk,
@@ -230,7 +69,8 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
   if (!last || threadIdx.x >= 64) return;
   __threadfence();  // every other block's result is visible after its arrival
   if (threadIdx.x == 0) S->arrive = 0;  // for the next launch (stream order)
-  ctl_body(S, H, result, nullptr, prm, status, t);
+  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
+  ctl_body(S, H, result, nullptr, prm, status, t, G);
 }
 
 // Row slabs over the peer-memory communicator: the reduction, the all-reduce of its nval sums
@@ -259,7 +99,8 @@ __global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
     return;
   }
   __threadfence();  // the combined values (other lanes' stores) before the control reads them
-  ctl_body(S, H, result, result_host, prm, status, t);
+  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
+  ctl_body(S, H, result, result_host, prm, status, t, G);
 }
 
 }  // namespace

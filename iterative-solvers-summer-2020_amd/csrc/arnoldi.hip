@@ -33,6 +33,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "arnctl_dev.h"
 #include "nk_device.h"
 #include "nk_kernels.h"
 #include "peer_dev.h"
@@ -438,6 +439,158 @@ __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int
 // sums each half's entries and adds the other half's sum (v_permlane32_swap); both halves then
 // hold v, y and w' of the wave's 64 columns, and each half takes the dot products of its own
 // entries (half 0 also w'.v, v.v, w'.w').
+// ------------------------------------------------------------------------------------------
+// Tail (device-side Arnoldi control, ArnoldiArgs::tail): the reduction + control launch that
+// would follow a fused launch, run by its last blocks instead (no kernel boundary in between).
+// Every active block counts in after writing its partial columns; the last kTailR to do so wait
+// until all have -- at most kTailR blocks wait, and every other block of the grid is running or
+// done (a launch is one resident round of blocks), so the wait ends -- and each reduces every
+// kTailR-th value over all partial columns in a fixed order (the same sums whichever blocks come
+// last).  The last reducer resets the counters, on a row slab all-reduces the values over the
+// peer-memory communicator, and runs the control of step t with its first wave, on the block's
+// LDS lag (free once the march is over) as the control's scratch.  A reducer that waits longer
+// than kTailWait gives up: the control never runs, and the host's wait for its status word ends
+// in an error (a fault, not a path this protocol takes).
+// Write-through (sc1) 8-B stores and loads: the hand-off between the blocks of one launch with
+// no release fence (MI355X_MICROARCH.md "Valid forms", first row: every byte stored sc1, every
+// storing wave drained, one agent-scope counter add per block; every load of the bytes sc1).
+// An agent-scope fence per block would write back its XCD's whole L2 (the launch's freshly
+// written output vectors) and invalidate its L1 under the blocks still streaming.
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(static_cast<long long>(
+      __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+#ifdef ARN_TAIL_PROBE  // timing build (scripts/dbg/tail_probe.py): stage times of the tails
+__device__ unsigned long long g_tail_probe[8];  // [0] tails, [1..5] summed stage ticks
+__device__ unsigned long long g_tail_first;     // wall clock of the current launch's first arrival
+#endif
+constexpr int kTailR = 8;
+constexpr int kTailC = (2 * kArnMaxNV + 3 + kTailR - 1) / kTailR;  // values per reducer
+constexpr uint64_t kTailWait = 1000000000ull;  // wall_clock64 ticks (100 MHz): 10 s
+template <int BS>
+__device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArnMaxNV + 1]) {
+  const ArnTail& T = A.tail;
+  __shared__ uint32_t ticket;
+  __shared__ bool ok;
+  __shared__ double redl[2 * kArnMaxNV + 3];  // the controller's copy of the step's values
+  drain_stores();  // this wave's partial columns (sc1 stores) have landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    ticket = __hip_atomic_fetch_add(&T.S->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+#ifdef ARN_TAIL_PROBE
+  const uint64_t p_arr = wall_clock64();
+  if (threadIdx.x == 0 && ticket == 0) g_tail_first = p_arr;
+#endif
+  const uint32_t total = uint32_t(nblocks);
+  const uint32_t R = total < uint32_t(kTailR) ? total : uint32_t(kTailR);
+  if (ticket < total - R) return;
+  const int rid = int(ticket - (total - R));
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    bool in = true;
+    while (__hip_atomic_load(&T.S->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) {
+      if (wall_clock64() - t0 > kTailWait) {
+        in = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    ok = in;
+  }
+  __syncthreads();
+  if (!ok) return;
+#ifdef ARN_TAIL_PROBE
+  const uint64_t p_all = wall_clock64();
+#endif
+  // values rid, rid + R, ..: each thread sums its columns of kTailC of them at a time (one round
+  // unless the grid has fewer than kTailR blocks), four columns per value in flight per iteration
+  const int64_t nw = A.pstride;
+  for (int q0 = 0, round = 0; rid + q0 * int(R) < T.nval; q0 += kTailC, ++round) {
+    double acc[kTailC];
+#pragma unroll
+    for (int q = 0; q < kTailC; ++q) acc[q] = 0.0;
+    int64_t b = threadIdx.x;
+    for (; b + 3 * BS < nw; b += 4 * BS) {
+      double x[kTailC][4];
+#pragma unroll
+      for (int q = 0; q < kTailC; ++q) {
+        const int c = rid + (q0 + q) * int(R);
+        const double* p = A.partial + int64_t(c < T.nval ? c : 0) * nw + b;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[q][u] = (c < T.nval) ? ld_sc1(p + u * BS) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < kTailC; ++q) acc[q] += ((x[q][0] + x[q][1]) + (x[q][2] + x[q][3]));
+    }
+    for (; b < nw; b += BS) {
+#pragma unroll
+      for (int q = 0; q < kTailC; ++q) {
+        const int c = rid + (q0 + q) * int(R);
+        acc[q] += (c < T.nval) ? ld_sc1(A.partial + int64_t(c) * nw + b) : 0.0;
+      }
+    }
+    const double s = block_reduce<kTailC, kTailC, BS>(acc, round & 1);
+    if (threadIdx.x < kTailC) {
+      const int c = rid + (q0 + int(threadIdx.x)) * int(R);
+      if (c < T.nval) st_sc1(T.result + c, s);
+    }
+  }
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    ok = __hip_atomic_fetch_add(&T.S->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == R - 1;
+  __syncthreads();
+  if (!ok || threadIdx.x >= 64) return;
+  // the controller (one wave): every reducer's values, sc1 loads into LDS
+  const int lane = threadIdx.x;
+  for (int i = lane; i < T.nval; i += 64) redl[i] = ld_sc1(T.result + i);
+  if (lane == 0) {  // for the next launch (stream order)
+    __hip_atomic_store(&T.S->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&T.S->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#ifdef ARN_TAIL_PROBE
+  const uint64_t p_red = wall_clock64();
+#endif
+  if (T.peer) {
+    if (!peer_allreduce_wave(T.pa, redl, T.nval, T.nval)) {
+      if (lane == 0) T.prm[kArnMaxNV + 3] = 1.0;  // the queued fused step does nothing
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    for (int i = lane; i < T.nval; i += 64) T.result[i] = redl[i];  // the combined values
+  }
+#ifdef ARN_TAIL_PROBE
+  const uint64_t p_ar = wall_clock64();
+#endif
+  ctl_body(T.S, T.H, redl, T.result_host, T.prm, T.status, T.t, G);
+#ifdef ARN_TAIL_PROBE
+  const uint64_t p_end = wall_clock64();
+  if (threadIdx.x == 0) {
+    const uint64_t f = g_tail_first;
+    atomicAdd(&g_tail_probe[0], 1ull);
+    atomicAdd(&g_tail_probe[1], (unsigned long long)(p_arr - f));  // first -> this block's arrival
+    atomicAdd(&g_tail_probe[2], (unsigned long long)(p_all - p_arr));  // -> all arrived
+    atomicAdd(&g_tail_probe[3], (unsigned long long)(p_red - p_all));  // -> all reduced
+    atomicAdd(&g_tail_probe[4], (unsigned long long)(p_ar - p_red));   // -> all-reduced
+    atomicAdd(&g_tail_probe[5], (unsigned long long)(p_end - p_ar));   // -> control done
+  }
+#endif
+}
+
 template <int NV, bool EXT, int PF, bool NT, bool MB, int WB>
 __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
@@ -926,15 +1079,21 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     for (int k = 0; k < NB; ++k) {
       const int e = 2 * k + hf;
       if (e < NV) {
-        p[int64_t(e) * nw] = aw[k];
-        p[int64_t(NV + 1 + e) * nw] = ag[k];
+        st_sc1(p + int64_t(e) * nw, aw[k]);
+        st_sc1(p + int64_t(NV + 1 + e) * nw, ag[k]);
       }
     }
     if (hf == 0) {
-      p[int64_t(NV) * nw] = t3[0];
-      p[int64_t(2 * NV + 1) * nw] = t3[1];
-      p[int64_t(2 * NV + 2) * nw] = t3[2];
+      st_sc1(p + int64_t(NV) * nw, t3[0]);
+      st_sc1(p + int64_t(2 * NV + 1) * nw, t3[1]);
+      st_sc1(p + int64_t(2 * NV + 2) * nw, t3[2]);
     }
+  }
+  if (A.tail.S) {  // uniform: the reduction + control of this step in the last blocks
+    constexpr bool fits = sizeof(lag) >= sizeof(double) * (kArnMaxNV + 1) * (kArnMaxNV + 1);
+    __shared__ double Gx[fits ? 1 : kArnMaxNV + 1][kArnMaxNV + 1];
+    arn_tail<64 * WB>(A, ngroups * A.nbands,
+                      fits ? reinterpret_cast<double (*)[kArnMaxNV + 1]>(&lag[0][0][0][0]) : Gx);
   }
 }
 
@@ -1329,12 +1488,18 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     ARN_CHK(A.pcol0 + gw < nw && (2 * int64_t(NV) + 2) * nw + A.pcol0 + gw < A.partial_cap);
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      p[int64_t(i) * nw] = aw[i];
-      p[int64_t(NV + 1 + i) * nw] = ag[i];
+      st_sc1(p + int64_t(i) * nw, aw[i]);
+      st_sc1(p + int64_t(NV + 1 + i) * nw, ag[i]);
     }
-    p[int64_t(NV) * nw] = aw[NV];
-    p[int64_t(2 * NV + 1) * nw] = aw[NV + 1];
-    p[int64_t(2 * NV + 2) * nw] = aw[NV + 2];
+    st_sc1(p + int64_t(NV) * nw, aw[NV]);
+    st_sc1(p + int64_t(2 * NV + 1) * nw, aw[NV + 1]);
+    st_sc1(p + int64_t(2 * NV + 2) * nw, aw[NV + 2]);
+  }
+  if (A.tail.S) {  // uniform: the reduction + control of this step in the last blocks
+    constexpr bool fits = sizeof(lag) >= sizeof(double) * (kArnMaxNV + 1) * (kArnMaxNV + 1);
+    __shared__ double Gx[fits ? 1 : kArnMaxNV + 1][kArnMaxNV + 1];
+    arn_tail<64 * W>(A, ngroups * A.nbands,
+                     fits ? reinterpret_cast<double (*)[kArnMaxNV + 1]>(&lag[0][0][0][0]) : Gx);
   }
 }
 
@@ -1398,6 +1563,11 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& oc
   if (A.pstride == 0) A.pstride = P.nw;
   if (A.pcol0 < 0 || A.pcol0 + P.nw > A.pstride ||
       A.pstride * (2 * int64_t(NV) + 3) > A.partial_cap)
+    return hipErrorInvalidValue;
+  // a tail reduces this launch's partials alone: one launch over the whole slab
+  if (A.tail.S && (A.pcol0 != 0 || A.pstride != P.nw || A.tail.nval != 2 * NV + 3 ||
+                   A.tail.nval > kRedMax || !A.tail.result || !A.tail.prm || !A.tail.status ||
+                   !A.tail.H || A.ctl != A.tail.prm || (A.tail.peer && !A.tail.result_host)))
     return hipErrorInvalidValue;
   A.strips = int(strips);
   A.nbands = int(P.nbands);
@@ -1607,6 +1777,16 @@ int arnoldi_mbox_mode() {
   const char* e = std::getenv("NKHIP_ARN_MBOX");
   return (e && *e) ? std::atoi(e) : 1;
 }
+
+#ifdef ARN_TAIL_PROBE
+extern "C" int nk_debug_tail_probe(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_probe), sizeof(g_tail_probe)) != hipSuccess)
+    return -1;
+  static const unsigned long long zero[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 bool arnoldi_wide(int nv) {
   static const bool on = env_int("NKHIP_ARN_WIDE", 1) != 0;

@@ -403,6 +403,7 @@ int NewtonKrylov::device_steps() {
   S.halt = 0;
   S.steps = 0;
   S.arrive = 0;
+  S.done = 0;
   volatile uint32_t* st = status_;
   for (int t = t0; t < S.m && t < kMaxVec + 2; ++t) st[t] = 0;
   std::atomic_thread_fence(std::memory_order_release);
@@ -416,6 +417,8 @@ int NewtonKrylov::device_steps() {
     double* v;
     bool fused;
     bool unfused;  // an unfused device step (update in place, JVP, multi-dot): nothing to rotate
+    bool ctl;      // the step queued a reduction + control launch (not the fused launch's tail)
+    bool red;      // ... and a separate reduction before it (the generic all-reduce path)
   };
   Rot rot[kMaxVec + 2];
   double cc[kMaxVec] = {};  // the launch arguments the parameter block overrides
@@ -432,7 +435,7 @@ int NewtonKrylov::device_steps() {
   // the fused step nv = t + 1 with the parameters control t writes, its reduction into the slot
   // of step t + 1 and the control of step t + 1
   auto issue = [&](int t) -> int {
-    rot[t] = Rot{Sv_, V_[t + 1], false, false};
+    rot[t] = Rot{Sv_, V_[t + 1], false, false, true, false};
     const int nval = 2 * (t + 2) + 1;
     const int slot = Engine::slot_mdot(t + 1);
     if (!P_.has_fused(t + 1)) {
@@ -461,6 +464,7 @@ int NewtonKrylov::device_steps() {
           return arn_reduce_ctl_launch(E_.partial(), nb, nval, E_.dres_mut(slot),
                                        E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
         });
+      rot[t].red = true;
       rc = E_.reduce_async(nb, nval, nval, slot, false);
       return rc ? rc : control(t + 1, true);
     }
@@ -468,25 +472,56 @@ int NewtonKrylov::device_steps() {
     for (int i = 0; i <= t; ++i) Vp[i] = V_[i];
     double* vout = Sv_;
     int64_t nw = 0;
+    // peer-memory slabs: the all-reduce runs inside a kernel (the fused launch's tail, or the
+    // reduction + all-reduce + control launch after it)
+    PeerArgs pa;
+    const bool have_pa = !one && peer_fuse_enabled() && E_.comm->take_allreduce(&pa, nval);
+    // the reduction + control in the fused launch's last blocks (NKHIP_ARN_TAIL=1; default: a
+    // launch of their own after it).  Ranks sharing one GPU keep the separate launch: with 8
+    // processes on one GPU, fused launches whose tails wait for the other ranks' all-reduce
+    // contributions stalled until the peer wait timed out (4 ranks ran), so the all-reduce inside
+    // a fused launch is kept to one rank per GPU (NKHIP_ARN_TAIL=2 forces it: tests).
+    ArnTail tl;
+    const char* te = std::getenv("NKHIP_ARN_TAIL");
+    const bool tail_env = te && (te[0] == '1' || te[0] == '2');
+    const bool want_tail = tail_env && (one || (have_pa && ((te && te[0] == '2') ||
+                                                            !E_.comm->group_shares_device())));
+    if (want_tail) {
+      tl.S = dS_;
+      tl.H = hS_;
+      tl.result = E_.dres_mut(slot);
+      tl.result_host = E_.hres_mut(slot);
+      tl.prm = prm_;
+      tl.status = status_;
+      tl.t = t + 1;
+      tl.nval = nval;
+      tl.peer = !one;
+      if (have_pa) tl.pa = pa;
+    }
+    bool tail_used = false;
     int rc = P_.fused_step(Vp, cc, t + 1, V_[t + 1], 1.0, X_, G0_, nullptr, 1.0, 1.0, vout,
-                           V_[t + 2], &nw, prm_);
+                           V_[t + 2], &nw, prm_, want_tail ? &tl : nullptr, &tail_used);
     if (rc) return rc;
     Sv_ = V_[t + 1];
     V_[t + 1] = vout;
     zp_[t + 1] = vout;
     rot[t].fused = true;
+    if (tail_used) {
+      rot[t].ctl = false;
+      return NK_OK;
+    }
     if (one)
       return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
         return arn_reduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
                                      E_.hres_mut(slot), dS_, hS_, prm_, status_, t + 1, E_.s);
       });
-    PeerArgs pa;  // peer-memory slabs: reduction, all-reduce and control in one launch
-    if (peer_fuse_enabled() && E_.comm->take_allreduce(&pa, nval))
+    if (have_pa)  // reduction, all-reduce and control in one launch
       return E_.launch(K_CTL, 8.0 * nw * nval, [&] {
         return arn_reduce_allreduce_ctl_launch(E_.partial(), nw, nval, E_.dres_mut(slot),
                                                E_.hres_mut(slot), pa, dS_, hS_, prm_, status_,
                                                t + 1, E_.s);
       });
+    rot[t].red = true;
     rc = E_.reduce_async(nw, nval, nval, slot, false);
     return rc ? rc : control(t + 1, true);
   };
@@ -512,8 +547,10 @@ int NewtonKrylov::device_steps() {
     if (next == t && next + 1 <= nvmax) rc = issue(next++);
   }
   // step t was handed back: the fused steps queued from t on do nothing; undo their rotations
-  int voided = 0, voided_unfused = 0;
+  int voided = 0, voided_unfused = 0, voided_ctl = 0, voided_red = 0;
   for (int u = next - 1; u >= t; --u) {
+    voided_ctl += rot[u].ctl ? 1 : 0;
+    voided_red += rot[u].red ? 1 : 0;
     if (rot[u].unfused) {  // its update and JVP saw the halt: V_[u+1], V_[u+2] untouched
       ++voided_unfused;
       continue;
@@ -526,11 +563,11 @@ int NewtonKrylov::device_steps() {
   // ... and their launches did no work: out of the kernel profile (the fused launches, and the
   // reduction + control launches each of those steps queued behind it)
   P_.void_fused_steps(voided);
-  E_.void_last(K_CTL, voided + voided_unfused);
+  E_.void_last(K_CTL, voided_ctl);
   E_.void_last(K_COMBO, voided_unfused);
   E_.void_last(K_USERF, voided_unfused);
   E_.void_last(K_MDOT, voided_unfused);
-  if (!one) E_.void_last(K_REDUCE, voided);
+  E_.void_last(K_REDUCE, voided_red);
   if (rc) return rc;
   // The voided reduction of slot_mdot(t + 1) may still write that pinned host slot after the
   // host resumes; drain the stream here so no later poll of the slot can meet a stale write

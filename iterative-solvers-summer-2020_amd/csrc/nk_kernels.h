@@ -10,11 +10,12 @@
 
 #include <cstdint>
 
+#include "peer_dev.h"  // PeerArgs: the peer-memory communicator's device-side arguments
+
 struct nk_comm;  // comm.h
 
 namespace nk {
 
-struct PeerArgs;  // peer_dev.h (the peer-memory communicator's device-side arguments)
 // Row slabs over the peer-memory communicator run their collectives inside the kernels around
 // them (arnoldi_edge_halo_launch, arn_reduce_allreduce_ctl_launch); NKHIP_PEER_FUSE=0 (read per
 // call) keeps the separate communicator launches.
@@ -178,6 +179,24 @@ struct SlabX {
   int* err = nullptr;  // pinned host error word of the communicator
   uint64_t wait_ticks = 0;  // bound of one wait (PeerArgs::wait_ticks)
 };
+struct ArnCtlState;
+// Tail of a fused launch under device-side Arnoldi control (arnoldi.hip "Tail"): the launch's
+// last blocks reduce its partials into `result` (and `result_host`), all-reduce them over the
+// peer-memory communicator on a row slab (peer), and the very last block runs the control of
+// step t on them -- the reduction + control launch that would otherwise follow, without its
+// kernel boundary.  S == nullptr: none.  S->arrive / S->done count the blocks (reset by the last).
+struct ArnTail {
+  ArnCtlState* S = nullptr;
+  ArnCtlState* H = nullptr;
+  double* result = nullptr;       // nval values (the multi-dot slot of step t)
+  double* result_host = nullptr;  // pinned copy (optional)
+  double* prm = nullptr;          // the parameter block the control writes (the next launch's ctl)
+  uint32_t* status = nullptr;
+  int t = 0;
+  int nval = 0;                   // 2 nv + 3
+  bool peer = false;
+  PeerArgs pa{};
+};
 struct ArnoldiArgs {
   int64_t ny = 0, nx = 0;
   int nv = 0;                      // basis vectors V_0..V_{nv-1}
@@ -238,6 +257,7 @@ struct ArnoldiArgs {
   int64_t mb_cap = 0;  // doubles at mb
   uint64_t mb_tag = 0;
   bool mb_recompute = false;  // test switch: every halo pair takes the mailbox's recompute path
+  ArnTail tail{};             // reduction + control in the launch's last blocks (S: on)
 };
 // doubles of mailbox a grid of ny rows and nx columns may need (any layout, any band count)
 inline int64_t arnoldi_mbox_elems(int64_t ny, int64_t nx) {
@@ -285,8 +305,9 @@ struct ArnCtlState {
   int32_t nv_max;      // the device issues fused steps up to this basis length
   int32_t halt;        // 0: the device continues; else 1 + the step it handed back
   int32_t steps;       // steps the device completed
-  uint32_t arrive;     // blocks of the running reduction that finished (arn_reduce_ctl_launch)
-  int32_t pad_;
+  uint32_t arrive;     // blocks of the running reduction that finished (arn_reduce_ctl_launch,
+                       // a fused launch's tail)
+  uint32_t done;       // a fused launch's tail: reducer blocks that finished
   double ptol, omega, lag_ratio2, pad2_;
   double sig[kMaxVec + 2];      // scale of basis vector i (kept raw: v_i = sig_i V_i)
   double rn[kMaxVec + 2];       // |V_i| raw

@@ -252,11 +252,14 @@ struct Problem {
                          const double* /*w*/, double /*tau*/, const double* /*x0*/,
                          const double* /*G0*/, const double* /*z*/, double /*zs*/, double /*sc*/,
                          double* /*out_v*/, double* /*out_w*/, int64_t* /*nwaves*/,
-                         const double* /*ctl*/) {
+                         const double* /*ctl*/, const ArnTail* /*tail*/ = nullptr,
+                         bool* /*tail_used*/ = nullptr) {
     return NK_EINVAL;
   }
   // ctl of fused_step (device-side Arnoldi control, nk_kernels.h ArnoldiArgs): c, tau, zs and sc
   // come from the device parameter block ctl, and the step does nothing when its halt entry is set.
+  // tail (optional): the step's reduction + control run in the launch's last blocks
+  // (ArnoldiArgs::tail) where the step is one launch; *tail_used says whether it did.
   // v (a pool vector) may enter the update of a later fused step: refresh its edge array.
   // eval()'s F and jvp()'s w come with fresh edge arrays (written by the pass itself); the solver
   // calls this after the other producers of update entries (its in-place combinations).

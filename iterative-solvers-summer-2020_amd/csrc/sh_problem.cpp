@@ -344,9 +344,16 @@ bool SHProblem::has_fused(int nv) const {
 int SHProblem::fused_step(const double* const* V, const double* c, int nv, const double* w,
                           double tau, const double* x0, const double* G0, const double* z,
                           double zs, double sc, double* out_v, double* out_w, int64_t* nwaves,
-                          const double* ctl) {
+                          const double* ctl, const ArnTail* tail, bool* tail_used) {
   ArnoldiArgs A;
   A.ctl = ctl;
+  if (tail_used) *tail_used = false;
+  // the step's reduction + control in the fused launch's last blocks (single-launch paths only)
+  auto with_tail = [&] {
+    if (!tail) return;
+    A.tail = *tail;
+    if (tail_used) *tail_used = true;
+  };
   A.ny = ny_;
   A.nx = nx_;
   A.nv = nv;
@@ -388,8 +395,10 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   }
   // algorithmic bytes per row: read V (nv), w, x0 (, z); write v, w'
   const double rowb = 8.0 * double(nx_) * (nv + 4 + (z ? 1 : 0));
-  if (!dist())
+  if (!dist()) {
+    with_tail();
     return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
+  }
 
   // Row slab: the stencil of rows 0, 1, ny-2, ny-1 needs u on the neighbours' edge rows, which
   // this step computes.  Every rank evaluates u on its own edge rows (a 4-row launch) and
@@ -420,6 +429,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
       A.yh_ld = nx_;
       last_split_ = false;
       edge_launched_ = false;
+      with_tail();
       return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
     }
     for (int i = 0; i <= nv + 1; ++i) A.HS[i] = nullptr;
@@ -481,6 +491,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
     A.yh = stage(A.x.me, pa.P, pa.max_nx, par, 0, 0);
     A.yh_ld = pa.max_nx;
     edge_launched_ = false;
+    with_tail();
     return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
   }
   if (!split && peer_fuse_enabled() && E_.comm->take_halo(&pa, nx_)) {
@@ -500,6 +511,7 @@ int SHProblem::fused_step(const double* const* V, const double* c, int nv, const
   }
   if (!split) {
     A.yh = yh_;
+    with_tail();
     return E_.launch(K_ARNOLDI, rowb * ny_, [&] { return arnoldi_launch(A, E_.s, nwaves); });
   }
   T.yh = Bm.yh = yh_;

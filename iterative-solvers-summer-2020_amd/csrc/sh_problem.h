@@ -27,7 +27,8 @@ class SHProblem final : public Problem {
   bool has_fused(int nv) const override;
   int fused_step(const double* const* V, const double* c, int nv, const double* w, double tau,
                  const double* x0, const double* G0, const double* z, double zs, double sc,
-                 double* out_v, double* out_w, int64_t* nwaves, const double* ctl) override;
+                 double* out_v, double* out_w, int64_t* nwaves, const double* ctl,
+                 const ArnTail* tail = nullptr, bool* tail_used = nullptr) override;
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
   int publish_edges(const double* v) override;

@@ -207,8 +207,10 @@ def test_edges_identical_solve(ny, nx, monkeypatch):
     assert pb["arnoldi_fused"]["launches"] > 0
 
 
-@pytest.mark.parametrize("ny,nx", [(64, 64), (128, 60), (96, 130), (256, 256), (40, 512)])
-def test_device_control_matches_host(ny, nx, monkeypatch):
+@pytest.mark.parametrize("ny,nx", [(64, 64), (128, 60), (96, 130), (256, 256), (40, 512),
+                                   (1024, 1024)])
+@pytest.mark.parametrize("tail", ["0", "1"])
+def test_device_control_matches_host(ny, nx, tail, monkeypatch):
     """Device-side Arnoldi control (arnctl.hip: the Givens update, residual test, Gram row and
     MGS coefficients computed by a one-wave kernel between the fused launches, handed back to the
     host loop at the stop): the same root as the host loop to 1e-8 of the state's scale, Newton
@@ -216,6 +218,7 @@ def test_device_control_matches_host(ny, nx, monkeypatch):
     monkeypatch.setenv("NKHIP_DEVCTL", "0")
     U0, a, sa, _ = _step(ny, nx, fused=True, steps=2)
     monkeypatch.setenv("NKHIP_DEVCTL", "1")
+    monkeypatch.setenv("NKHIP_ARN_TAIL", tail)  # 1: reduction + control in the fused launch's tail
     _, b, sb, pb = _step(ny, nx, fused=True, steps=2)
     assert all(s["n_device_steps"] == 0 for s in sa)
     assert sum(s["n_device_steps"] for s in sb) > 0

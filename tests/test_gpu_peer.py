@@ -98,18 +98,22 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,N,steps,xk", [(2, 128, 2, "auto"), (2, 61, 1, "auto"),
-                                             (3, 96, 1, "auto"), (4, 128, 1, "auto"),
-                                             (8, 256, 1, "auto"), (2, 128, 2, "1"),
-                                             (3, 96, 1, "1"), (4, 256, 1, "1")])
-def test_peer_processes_match_single_slab(world, N, steps, xk, tmp_path):
+@pytest.mark.parametrize("world,N,steps,xk,tail", [
+    (2, 128, 2, "auto", None), (2, 61, 1, "auto", None), (3, 96, 1, "auto", None),
+    (4, 128, 1, "auto", None), (8, 256, 1, "auto", None), (2, 128, 2, "1", None),
+    (3, 96, 1, "1", None), (4, 256, 1, "1", None), (2, 128, 2, "auto", "2"),
+    (4, 256, 1, "auto", "2")])
+def test_peer_processes_match_single_slab(world, N, steps, xk, tail, tmp_path):
     """``world`` processes on one GPU, one slab each, the peer buffers mapped through IPC
     (dmabuf) handles: the gathered slabs equal the single-slab steps.  World 2 has prev == next
     (both halo directions go to one peer); N = 61 takes the point kernel (odd nx); 8 x 256 runs
     the fused Arnoldi step on 32-row slabs with the device-side control.  xk = "1": the fused
     kernel's edge bands run the slab exchange themselves (NKHIP_SLAB_XK=1 forces it although the
     ranks share this GPU: the ranks' grids then wait on each other's edge bands, which always
-    progresses -- publishing never waits -- but slowly; "auto" takes the edge + halo kernel)."""
+    progresses -- publishing never waits -- but slowly; "auto" takes the edge + halo kernel).
+    tail = "2": the fused launches' tails run the reduction, the all-reduce and the control
+    although the ranks share this GPU (NKHIP_ARN_TAIL=2; by default they do so only with one
+    rank per GPU)."""
     import subprocess
     U0 = np.random.default_rng(2020).standard_normal((N, N))
     import nkhip
@@ -129,6 +133,8 @@ def test_peer_processes_match_single_slab(world, N, steps, xk, tmp_path):
                    OUT_DIR=str(tmp_path), LOCAL_RANK="0")
         if xk != "auto":
             env["NKHIP_SLAB_XK"] = xk
+        if tail is not None:
+            env["NKHIP_ARN_TAIL"] = tail
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -139,8 +145,8 @@ def test_peer_processes_match_single_slab(world, N, steps, xk, tmp_path):
             for q in procs:
                 q.kill()
             raise
-    for p, o in zip(procs, outs):
-        assert p.returncode == 0, o[-3000:]
+    assert all(p.returncode == 0 for p in procs), "\n".join(
+        f"--- rank {r} rc {p.returncode}\n{o[-1500:]}" for r, (p, o) in enumerate(zip(procs, outs)))
     got = np.concatenate([np.load(tmp_path / f"slab{r}.npy") for r in range(world)], axis=0)
     assert np.abs(got - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max()), outs
 
