@@ -611,13 +611,17 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
     neighbours' halo slots, the fused pass forms u on its halo rows itself, nothing is exchanged
     in between; edge_halo (NKHIP_SLAB_PUSH=0): a 4-row edge kernel exchanges u on the slab's edge
     rows before the fused pass; in_kernel (NKHIP_SLAB_XK=2, =1 when the ranks share a GPU): the
-    fused pass's edge bands exchange them themselves.  Returns (record, a, b), the trajectory
-    advanced."""
-    names = ("pushed", "edge_halo", "in_kernel")
-    env = {"pushed": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0"},
-           "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0"},
-           "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2"}}
-    old = {k_: os.environ.get(k_) for k_ in ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK")}
+    fused pass's edge bands exchange them themselves; pushed_tail (NKHIP_ARN_TAIL=1): pushed,
+    with each step's reduction + all-reduce + control in the fused launch's last blocks (one rank
+    per GPU only: with ranks sharing a GPU it is the pushed path).  Returns (record, a, b), the
+    trajectory advanced."""
+    names = ("pushed", "edge_halo", "in_kernel", "pushed_tail")
+    env = {"pushed": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
+           "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
+           "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2",
+                         "NKHIP_ARN_TAIL": "0"},
+           "pushed_tail": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "1"}}
+    old = {k_: os.environ.get(k_) for k_ in ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK", "NKHIP_ARN_TAIL")}
     acc = {n_: [0.0, 0] for n_ in names}
     try:
         for i in range(len(names) * rounds):
