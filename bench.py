@@ -623,6 +623,7 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
            "pushed_tail": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "1"}}
     old = {k_: os.environ.get(k_) for k_ in ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK", "NKHIP_ARN_TAIL")}
     acc = {n_: [0.0, 0] for n_ in names}
+    failed = None
     try:
         for i in range(len(names) * rounds):
             name = names[i % len(names)]
@@ -630,11 +631,18 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
             dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            model.step(a, out=b)
-            torch.cuda.synchronize()
-            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
+            err = 0.0
+            try:  # a variant that fails ends the comparison on every rank, not the bench line
+                model.step(a, out=b)
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001 (nkhip.NKError and HIP errors alike)
+                err, failed = 1.0, f"{name}: {e}"
+            t = torch.tensor([time.perf_counter() - t0, err], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            acc[name][0] += float(t.item())
+            if float(t[1].item()) > 0:
+                failed = failed or f"{name}: failed on another rank"
+                break
+            acc[name][0] += float(t[0].item())
             acc[name][1] += model.last_stats["njvp"]
             a, b = b, a
     finally:
@@ -644,6 +652,8 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
             else:
                 os.environ[k_] = v
     rec = {f"{k_}_ms_per_arnoldi": round(1e3 * v[0] / max(v[1], 1), 4) for k_, v in acc.items()}
+    if failed:
+        rec["failed"] = failed
     rec.update({"steps_each": rounds, "arnoldi_steps": {k_: v[1] for k_, v in acc.items()},
                 "what": "rotating time steps after the timed region; max over ranks of each "
                         "step's wall time / its Arnoldi steps"})
