@@ -517,11 +517,22 @@ def copy_bandwidth(n, reps=20):
                     "after the timed region"}
 
 
-def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cuda", allow_rccl=True):
-    """The peer-memory communicator, verified before it is used: one all-reduce and one halo
-    exchange of known values through it, at the full row width (nk_comm_selftest; device waits
-    are bounded).  If any rank cannot create, map or verify it, every rank falls back to RCCL
-    (stderr says so) -- or fails, when the ranks share a device (RCCL takes one rank per GPU)."""
+def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cpu", allow_rccl=True):
+    """The peer-memory communicator, verified before it is used, at the full row width, with
+    bounded device waits.  Two collectives, each agreed on over the gloo side channel:
+      1. nk_comm_selftest -- one all-reduce and one halo exchange of known values.  If any rank
+         cannot create, map or verify the group, every rank falls back to RCCL (stderr says so)
+         -- or fails, when the ranks share a device (RCCL takes one rank per GPU);
+      2. nk_comm_selftest_push -- the pushed-halo-rows protocol the slab solver uses by default
+         (push into the neighbours' halo slots, system-scope fence, no flag, one all-reduce, read
+         back, host check).  If it fails on any rank, every rank runs the edge + halo exchange
+         path instead (NKHIP_SLAB_PUSH=0), which step 1 verified.
+    Returns (comm, check): check records both outcomes and the slab path taken."""
+    def agree(v):
+        t = torch.tensor([int(v)], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
     comm, ok = None, 1
     try:
         comm = nkhip.PeerComm.from_torch_distributed(max_nx=max_nx)
@@ -529,10 +540,23 @@ def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cuda", allow_rccl=True):
     except Exception as e:  # noqa: BLE001 - any failure means: use RCCL instead
         print(f"peer-memory communicator unavailable: {e}", file=sys.stderr)
         ok = 0
-    flag = torch.tensor([ok], dtype=torch.int32, device=coll_dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if int(flag.item()) == 1:
-        return comm
+    if agree(ok) == 1:
+        push = comm.selftest_push(max_nx)  # True / False / None (no slots: nothing to check)
+        push_ok = agree(push is not False)
+        check = {"selftest": "ok"}
+        if push is None:
+            check["pushed_rows_selftest"] = "n/a (no halo slots)"
+            check["slab_path"] = "edge_halo"
+        elif push_ok == 1:
+            check["pushed_rows_selftest"] = "ok"
+            check["slab_path"] = "pushed"
+        else:
+            print("pushed-halo-rows self-test failed on some rank: every rank takes the edge + "
+                  "halo exchange path (NKHIP_SLAB_PUSH=0)", file=sys.stderr)
+            os.environ["NKHIP_SLAB_PUSH"] = "0"
+            check["pushed_rows_selftest"] = "failed on some rank"
+            check["slab_path"] = "edge_halo"
+        return comm, check
     print("peer-memory communicator failed its self-test on some rank"
           + (": using RCCL" if allow_rccl else ""), file=sys.stderr)
     if comm is not None:
@@ -540,7 +564,92 @@ def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cuda", allow_rccl=True):
         comm.close()
     if not allow_rccl:
         raise RuntimeError("peer-memory communicator failed and the ranks share a device")
-    return nkhip.RcclComm.from_torch_distributed()
+    return nkhip.RcclComm.from_torch_distributed(), {"selftest": "failed on some rank: RCCL",
+                                                     "slab_path": "edge_halo"}
+
+
+def slab_residual_max(nkhip, dist, torch, u1, u0, n, rank, world, h, r, k, g):
+    """The oracle residual (sh_scipy_nk.py:47-49) of a row-slab state, max over the whole grid,
+    without gathering it: each rank pads its slab of U[s+1] and U[s] with the ring neighbours'
+    two edge rows (gloo all_gather of 4 rows per rank), evaluates the oracle's periodic stencil
+    on the padded block -- exact on its interior rows -- on the host, and the max goes over the
+    ranks (every rank gets it)."""
+    import numpy as np
+
+    from oracle import sh_oracle
+    ny = u1.shape[0]
+    out = []
+    for x in (u1, u0):
+        x = x.cpu()
+        edge = torch.cat([x[:2], x[-2:]]).to(torch.float64)
+        parts = [torch.empty_like(edge) for _ in range(world)]
+        dist.all_gather(parts, edge)
+        prev, nxt = parts[(rank - 1) % world], parts[(rank + 1) % world]
+        out.append(torch.cat([prev[2:], x, nxt[:2]]).numpy())
+    F = sh_oracle.residual(out[0].reshape(-1), out[1].reshape(-1), ny + 4, n, h, r, k, g)
+    worst = torch.tensor([float(np.abs(F.reshape(ny + 4, n)[2:-2]).max())], dtype=torch.float64)
+    del F, out
+    dist.all_reduce(worst, op=dist.ReduceOp.MAX)
+    return float(worst.item())
+
+
+def config5_slabs(nkhip, dist, torch, comm, check, n5, rank, world, one_device, steps=1,
+                  warmup=1):
+    """Config 5 on the N ranks of this job: the 16384^2 grid (d = 0.625 N, k, r, g and seed as the
+    headline) cut into the same row slabs over the same kind of communicator (a peer-memory group
+    of the full 16384-column width, verified as the headline's), ``warmup`` untimed + ``steps``
+    timed time steps, max over ranks; the whole grid's oracle residual of the last step
+    (slab_residual_max).  One point of the 1/2/4/8-GPU curve per driver run.  Returns (record,
+    comm): the communicator the caller closes."""
+    import numpy as np
+    if comm is not None and type(comm).__name__ == "PeerComm":
+        comm.close()  # the headline's group is 4096 columns wide
+        dist.barrier()
+        comm, check = peer_or_rccl(nkhip, dist, torch, n5, "cpu", allow_rccl=not one_device)
+    h, k, r, g = 0.625, 0.2, 0.01, 1.0
+    row0, ny = nkhip.slab_rows(n5, rank, world)
+    # the first row0 + ny rows of default_rng(2020).standard_normal((n5, n5)): the same numbers
+    U = np.random.default_rng(2020).standard_normal((row0 + ny, n5))[row0:]
+    a = torch.as_tensor(np.ascontiguousarray(U), device="cuda")
+    del U
+    b = torch.empty_like(a)
+    dist.barrier()
+    m = nkhip.SwiftHohenberg(N=n5, d=h * n5, k=k, r=r, g=g, comm=comm, ny_local=ny)
+    for _ in range(warmup):
+        m.step(a, out=b)
+        a, b = b, a
+    tot = {"nit": 0, "njvp": 0}
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.step(a, out=b)
+        for key in tot:
+            tot[key] += m.last_stats[key]
+        a, b = b, a
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    res = slab_residual_max(nkhip, dist, torch, a, b, n5, rank, world, h, r, k, g)
+    dist.barrier()
+    m.close()
+    del a, b
+    torch.cuda.empty_cache()
+    rec = {"workload": f"swift_hohenberg_cn_newton_krylov_{n5}x{n5}", "grid": n5,
+           "n_gpus": world, "steps": steps, "warmup": warmup,
+           "steps_per_s": round(steps / dt, 4),
+           "ms_per_arnoldi_step": round(1e3 * dt / max(tot["njvp"], 1), 4),
+           "newton_its_per_step": tot["nit"] / steps,
+           "arnoldi_steps_per_step": tot["njvp"] / steps,
+           "final_step_residual": res, "f_tol": float(np.finfo(float).eps ** (1 / 3)),
+           "comm": type(comm).__name__, "comm_check": check,
+           "what": "row slabs of the 16384^2 grid on this job's ranks after the headline; "
+                   "final_step_residual = oracle residual of the last step over the whole grid "
+                   "(padded slabs on the host, max over ranks)"}
+    if one_device:
+        rec["ranks_on_one_device"] = True
+    return rec, comm
 
 
 def load_traffic():
@@ -604,7 +713,7 @@ def self_launch(n):
     return 0
 
 
-def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
+def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pushed_ok=True):
     """N > 1, after the timed region: the slab paths of the fused Arnoldi step, rotating one time
     step each (``rounds`` of each), as ms per Arnoldi step (max over ranks of each step's wall
     time / its Arnoldi steps).  pushed (the default): every producer writes its edge rows into the
@@ -616,6 +725,8 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
     per GPU only: with ranks sharing a GPU it is the pushed path).  Returns (record, a, b), the
     trajectory advanced."""
     names = ("pushed", "edge_halo", "in_kernel", "pushed_tail")
+    if not pushed_ok:  # the pushed-halo-rows self-test failed (or there are no slots)
+        names = ("edge_halo", "in_kernel")
     env = {"pushed": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
            "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
            "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2",
@@ -652,6 +763,8 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
             else:
                 os.environ[k_] = v
     rec = {f"{k_}_ms_per_arnoldi": round(1e3 * v[0] / max(v[1], 1), 4) for k_, v in acc.items()}
+    if not pushed_ok:
+        rec["skipped"] = "pushed, pushed_tail (the pushed-halo-rows self-test did not pass)"
     if failed:
         rec["failed"] = failed
     rec.update({"steps_each": rounds, "arnoldi_steps": {k_: v[1] for k_, v in acc.items()},
@@ -661,6 +774,7 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch):
 
 
 def main():
+    rc = 0
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -680,7 +794,7 @@ def main():
     one_device = world > 1 and os.environ.get("NKHIP_BENCH_ONE_DEVICE") == "1"
     device = 0 if one_device else local
     torch.cuda.set_device(device)
-    comm = None
+    comm, comm_check = None, None
     use_dist = world > 1 or args.rccl_self or args.peer_self
     # torch.distributed is only the side channel (IPC handle / RCCL unique-id exchange, barriers,
     # the max over ranks of the timed region, the final gather): gloo on host tensors.  The
@@ -697,7 +811,8 @@ def main():
         if args.rccl_self or (world > 1 and args.comm == "rccl" and not args.peer_self):
             comm = nkhip.RcclComm.from_torch_distributed()
         else:
-            comm = peer_or_rccl(nkhip, dist, torch, args.n, coll_dev, allow_rccl=not one_device)
+            comm, comm_check = peer_or_rccl(nkhip, dist, torch, args.n, coll_dev,
+                                            allow_rccl=not one_device)
 
     n = args.n
     h, k, r, g = 0.625, 0.2, 0.01, 1.0
@@ -767,7 +882,19 @@ def main():
     slab_ab = None
     if world > 1 and args.slab_ab > 0:
         slab_ab, a, b = slab_exchange_ab(model, a, b, args.slab_ab, one_device, dist, coll_dev,
-                                         torch)
+                                         torch, pushed_ok=(comm_check or {}).get("slab_path")
+                                         == "pushed")
+    # config 5 on this job's ranks (N > 1): the point of the 16384^2 curve; at N = 1 it runs
+    # below, in other_configs.config5_1gpu
+    c5 = None
+    if world > 1 and args.extra == "on":
+        model.close()
+        model = None
+        del a, b
+        torch.cuda.empty_cache()
+        c5, comm = config5_slabs(nkhip, dist, torch, comm, comm_check,
+                                 int(os.environ.get("NKHIP_BENCH_CONFIG5_N", "16384")), rank,
+                                 world, one_device)
 
     if rank == 0:
         steps_per_s = args.steps / elapsed
@@ -810,7 +937,8 @@ def main():
         final_check = {"max_abs_residual": float(np.abs(F_last).max()),
                        "f_tol": float(np.finfo(float).eps ** (1 / 3)),
                        "what": "oracle residual (sh_scipy_nk.py:47-49) of the last timed step, "
-                               "evaluated on the host over the whole grid"}
+                               "evaluated on the host over the whole grid; above f_tol the "
+                               "bench exits non-zero after printing its line"}
         del F_last
         jvp_name = "sh_fdjvp" if args.jvp == "fd" else "sh_ajvp"
         kernel_ms = sum(v["ms_est"] for v in ker.values())
@@ -832,6 +960,7 @@ def main():
                        "f_tol": "scipy default eps^(1/3) (max-norm)", "inner_m": 30,
                        "outer_k": 10, "parallelism": f"row-slab x{world}",
                        "comm": (type(comm).__name__ if comm is not None else "none")},
+            "comm_check": comm_check,
             "newton_its_per_s": round(tot["nit"] / elapsed, 3),
             "jvps_per_s": round(tot["njvp"] / elapsed, 2),
             "per_step": {k_: v / args.steps for k_, v in tot.items()},
@@ -898,6 +1027,8 @@ def main():
                 "bar": "1e-5 * max(1, |U|) (default f_tol)"}
             del ua, ub, u_cpu
             out["cpu_baseline"] = rec
+        if c5 is not None:
+            out["other_configs"] = {"config5": c5}
         if world == 1 and args.extra == "on":
             out["other_configs"] = {"config2": config2_lap5(rocprof=args.pmc == "auto"),
                                     "config3": config3_droplet(),
@@ -905,14 +1036,25 @@ def main():
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),
                                     "droplet_init": config_droplet_init()}
         print(json.dumps(out), flush=True)
+        # a wrong answer fails the run (sh_scipy_nk.py:47-49: the step is a root to f_tol in the
+        # max norm; the slack covers the oracle's own rounding, ~1e-14 at these magnitudes)
+        for what, v, tol in (("headline", final_check["max_abs_residual"], final_check["f_tol"]),
+                             ("config5", (c5 or {}).get("final_step_residual", 0.0),
+                              final_check["f_tol"])):
+            if not v <= tol + 1e-12:
+                print(f"bench: {what} final-step residual {v:.3e} exceeds f_tol {tol:.3e}",
+                      file=sys.stderr)
+                rc = 3
     if use_dist:
         dist.barrier()  # no rank frees its communicator buffers while a peer may still use them
-    model.close()
+    if model is not None:
+        model.close()
     if comm is not None:
         comm.close()
     if use_dist:
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

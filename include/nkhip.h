@@ -221,6 +221,15 @@ int nk_comm_abort(nk_comm* c);
  * checked on the host; every rank calls it (a collective).  NK_OK, or NK_ECOMM when a value did
  * not arrive intact (bench.py falls back from the peer-memory communicator to RCCL on that). */
 int nk_comm_selftest(nk_comm* c, int64_t nx, void* stream);
+/* The pushed-halo-rows protocol the slab solver uses by default on the peer-memory
+ * communicator, exactly as the solver runs it: every rank pushes 4 rows of
+ * known codes into its ring neighbours' halo slots (push kernel, system-scope fence, no flag),
+ * passes ONE all-reduce, then reads its own slots back in a kernel and checks them on the host;
+ * every rank calls it (a collective).  NK_OK; NK_ECOMM when a row did not arrive intact (bench.py
+ * then runs the edge + halo exchange path, NKHIP_SLAB_PUSH=0, on every rank); NK_EINVAL on every
+ * rank when some rank's communicator has no halo slots (RCCL, loopback) or a stepper holds them.
+ * Replaces no reference interface: the check before the multi-GPU path is trusted. */
+int nk_comm_selftest_push(nk_comm* c, int64_t nx, void* stream);
 
 /* ---------------- Swift-Hohenberg implicit time step (the north-star path) ---------------- */
 /* A stepper for one row slab [row0, row0+ny_local) of an ny_global x nx periodic grid.

@@ -296,7 +296,7 @@ __device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0
 // the communicator's error word; the host sees it at its next synchronisation.
 template <int NV>
 __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW, int h0,
-                                double a_tau) {
+                                double a_tau, bool top, bool bot) {
   const SlabX& X = A.x;
   const int64_t nx = A.nx, ny = A.ny;
   const bool first = band == 0, last = band == int64_t(A.nbands) - 1;
@@ -328,8 +328,10 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
   const int64_t cl = ((B0 - 2 + nx) % nx) / kXChunk, c0 = B0 / kXChunk;
   const int64_t c1 = (cend - 1) / kXChunk, cr = ((B0 + BW) % nx) / kXChunk;
   const int64_t nown = c1 - c0 + 1;
+  // every band whose stencil reaches a halo row waits for it (`top`: rows -2, -1; `bot`: rows ny,
+  // ny+1), not only the first and last: a last band of one row leaves row ny to the band before
   for (int side = 0; side < 2; ++side) {
-    if (side == 0 ? !first : !last) continue;
+    if (side == 0 ? !top : !bot) continue;
     const int t = int(threadIdx.x);
     if (t < nown + 2) {
       const int64_t ch = (t == 0) ? cl : ((t == 1) ? cr : c0 + (t - 2));
@@ -359,10 +361,9 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
 // no block waits for another rank.  (A halo column shared with the neighbouring block is written
 // by both with the same bits.)
 template <int NV>
-__device__ void slab_push_prologue(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW,
-                                   int h0, const double* cst, double a_tau) {
+__device__ void slab_push_prologue(const ArnoldiArgs& A, bool first, bool last, int64_t B0,
+                                   int64_t BW, int h0, const double* cst, double a_tau) {
   const int64_t nx = A.nx, ld = A.hs_ld;
-  const bool first = band == 0, last = band == int64_t(A.nbands) - 1;
   double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
   constexpr int NE = NV + 1;
   // (row, column) items per thread and round: each round's loads are in flight together (one
@@ -450,7 +451,11 @@ __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int
 // peer-memory communicator, and runs the control of step t with its first wave, on the block's
 // LDS lag (free once the march is over) as the control's scratch.  A reducer that waits longer
 // than kTailWait gives up: the control never runs, and the host's wait for its status word ends
-// in an error (a fault, not a path this protocol takes).
+// in an error (a fault, not a path this protocol takes): the reducer sets the halt word (the
+// queued launches do nothing) and, on a slab, the communicator's error word.  The wait bound is
+// ArnTail::wait_ticks (device_wait_ticks, from the wall-clock rate); device_steps resets the
+// arrival counters before every run of device steps, so a launch that gave up leaves no count
+// behind for the next run.
 // Write-through (sc1) 8-B stores and loads: the hand-off between the blocks of one launch with
 // no release fence (MI355X_MICROARCH.md "Valid forms", first row: every byte stored sc1, every
 // storing wave drained, one agent-scope counter add per block; every load of the bytes sc1).
@@ -474,7 +479,6 @@ __device__ unsigned long long g_tail_first;     // wall clock of the current lau
 #endif
 constexpr int kTailR = 8;
 constexpr int kTailC = (2 * kArnMaxNV + 3 + kTailR - 1) / kTailR;  // values per reducer
-constexpr uint64_t kTailWait = 1000000000ull;  // wall_clock64 ticks (100 MHz): 10 s
 template <int BS>
 __device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArnMaxNV + 1]) {
   const ArnTail& T = A.tail;
@@ -498,7 +502,7 @@ __device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArn
     const uint64_t t0 = wall_clock64();
     bool in = true;
     while (__hip_atomic_load(&T.S->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) {
-      if (wall_clock64() - t0 > kTailWait) {
+      if (wall_clock64() - t0 > T.wait_ticks) {
         in = false;
         break;
       }
@@ -507,7 +511,14 @@ __device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArn
     ok = in;
   }
   __syncthreads();
-  if (!ok) return;
+  if (!ok) {  // a fault, not a path of this protocol: halt the queued launches and report it
+    if (threadIdx.x == 0) {
+      st_sc1(T.prm + kArnMaxNV + 3, 1.0);
+      if (T.peer && T.pa.err)
+        __hip_atomic_store(T.pa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
 #ifdef ARN_TAIL_PROBE
   const uint64_t p_all = wall_clock64();
 #endif
@@ -1007,9 +1018,14 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     h2q.y = h2q.y + h.y;
   };
 
-  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau);  // uniform per block
-  const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
-  if (edge_band) slab_push_prologue<NV>(A, band, B0, BW, 0, cst, a_tau);  // uniform per block
+  // bands whose stencil reaches the slab's halo rows (rows -2, -1 / ny, ny+1): the first and
+  // the last, and the one before a last band of a single row.  Each computes (or waits for) the
+  // halo rows it reads itself -- the same bits from every band -- and fences the edge rows it
+  // pushes (a band ending at ny - 1 pushes row ny - 2)
+  const bool top = r0 < 2, bot = r1 + 2 > ny;
+  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau, top, bot);  // uniform per block
+  const bool edge_band = A.hs_ld > 0 && (top || bot);
+  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, 0, cst, a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
     // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
@@ -1437,9 +1453,10 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     h2q.y = h2q.y + h.y;
   };
 
-  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau);  // uniform per block
-  const bool edge_band = A.hs_ld > 0 && (band == 0 || band == int64_t(A.nbands) - 1);
-  if (edge_band) slab_push_prologue<NV>(A, band, B0, BW, NV + 1, cst, a_tau);
+  const bool top = r0 < 2, bot = r1 + 2 > ny;  // as in arnoldi_kernel
+  if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau, top, bot);  // uniform per block
+  const bool edge_band = A.hs_ld > 0 && (top || bot);
+  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, NV + 1, cst, a_tau);
   if (nrows > 0) {
     Slot P[2];
     load(P[0], r0 - 2);

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -432,6 +433,101 @@ int nk_comm_selftest(nk_comm* c, int64_t nx, void* stream) {
     for (int64_t j = 0; j < nx; ++j)
       if (lo[row * nx + j] != code(prev, 2 + row, j) || hi[row * nx + j] != code(next, row, j))
         return NK_ECOMM;
+  return NK_OK;
+}
+
+namespace {
+// plain global loads, as the fused kernel's edge bands read the halo slots (slab_push_prologue)
+__global__ void slot_read_kernel(const double* src, double* dst, int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+}  // namespace
+
+// The pushed-halo-rows protocol exactly as the solver runs it (arnoldi.hip "Pushed halo rows"):
+// every rank clears its own slots, passes an all-reduce, pushes a 4-row slab of known codes into
+// its ring neighbours' slots with push_rows_launch (system-scope fence, no flag), passes ONE
+// all-reduce, then reads its own slots back with plain loads in a kernel and checks them on the
+// host -- rows 0, 1 the previous rank's rows ny-2, ny-1, rows 2, 3 the next rank's rows 0, 1.
+// Slots 0 and count-1 are checked.  NKHIP_PEER_SELFTEST_BREAK_PUSH=<rank>: that rank pushes
+// wrong codes (fault injection for the fallback path).
+int nk_comm_selftest_push(nk_comm* c, int64_t nx, void* stream) {
+  if (!c || nx < 1) return NK_EINVAL;
+  const hipStream_t s = S(stream);
+  nk_halo_slots sl;
+  static const char owner = 0;  // a claim of its own: refused while a stepper holds the slots
+  const bool claimed = c->claim_slots(&owner, &sl);
+  struct Release {
+    nk_comm* c;
+    bool on;
+    ~Release() {
+      if (on) c->release_slots(&owner);
+    }
+  } rel{c, claimed};
+  const bool have = claimed && sl.ld >= nx && sl.count >= 1;
+  const int P = c->size(), r = c->rank();
+  const int64_t ny = 4;
+  const int64_t slots[2] = {0, sl.count - 1};
+  const char* be = std::getenv("NKHIP_PEER_SELFTEST_BREAK_PUSH");
+  const bool broken = be && *be && std::atoi(be) == r;
+  auto code = [&](int q, int64_t slot, int64_t row, int64_t j) {
+    return 1e9 * (q + 1) + 1e6 * slot + double(row * nx + j);
+  };
+  const int64_t nslot = have ? 4 * sl.ld : 0;
+  std::vector<double> h(2 * ny * nx + 2 * nslot + 2);
+  h[2 * ny * nx + 2 * nslot] = have ? 0.0 : 1.0;  // max over ranks: some rank has no slots
+  double* d = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&d), h.size() * sizeof(double)) != hipSuccess)
+    return NK_EHIP;
+  double* vsrc = d;                  // [2][ny][nx] the pushed slabs
+  double* rd = d + 2 * ny * nx;      // [2][4][ld] the slots read back
+  double* ar = rd + 2 * nslot;       // 2 values for the all-reduces
+  for (int k = 0; k < 2; ++k)
+    for (int64_t row = 0; row < ny; ++row)
+      for (int64_t j = 0; j < nx; ++j)
+        h[(k * ny + row) * nx + j] = code(r, slots[k], row, j) + (broken ? 0.5 : 0.0);
+  int rc = NK_OK;
+  auto ok = [&](hipError_t e) {
+    if (!rc && e != hipSuccess) rc = NK_EHIP;
+  };
+  for (int k = 0; k < 2 && have; ++k)
+    ok(hipMemsetAsync(sl.mine + slots[k] * 4 * sl.ld, 0xff, sizeof(double) * nslot, s));  // NaN
+  ok(hipMemcpyAsync(d, h.data(), sizeof(double) * (2 * ny * nx + 2 * nslot + 2),
+                    hipMemcpyHostToDevice, s));
+  // every rank cleared its slots before any pushes, and every rank has slots
+  if (!rc) rc = c->allreduce(ar, 0, 2, s);
+  double any_without = 1.0;
+  if (!rc && (hipMemcpyAsync(&any_without, ar, sizeof(double), hipMemcpyDeviceToHost, s) !=
+                  hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+    rc = NK_EHIP;
+  if (!rc && any_without != 0.0) rc = NK_EINVAL;  // on every rank alike: nothing to check
+  for (int k = 0; k < 2 && !rc; ++k)
+    ok(push_rows_launch(vsrc + k * ny * nx, sl.prev + slots[k] * 4 * sl.ld,
+                        sl.next + slots[k] * 4 * sl.ld, ny, nx, sl.ld, s));
+  if (!rc) rc = c->allreduce(ar, 1, 2, s);  // the one all-reduce that orders the pushes
+  for (int k = 0; k < 2 && !rc; ++k) {
+    hipLaunchKernelGGL(slot_read_kernel, dim3(unsigned((nslot + 255) / 256)), dim3(256), 0, s,
+                       sl.mine + slots[k] * 4 * sl.ld, rd + k * nslot, nslot);
+    ok(hipGetLastError());
+  }
+  if (!rc && (hipMemcpyAsync(h.data(), rd, sizeof(double) * 2 * nslot, hipMemcpyDeviceToHost, s) !=
+                  hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+    rc = NK_EHIP;
+  (void)hipFree(d);
+  if (rc) return rc;
+  if (c->failed()) return NK_ECOMM;
+  const int prev = (r - 1 + P) % P, next = (r + 1) % P;
+  for (int k = 0; k < 2; ++k) {
+    const double* m = h.data() + k * nslot;
+    for (int64_t row = 0; row < 4; ++row)
+      for (int64_t j = 0; j < nx; ++j) {
+        const double want = row < 2 ? code(prev, slots[k], ny - 2 + row, j)
+                                    : code(next, slots[k], row - 2, j);
+        if (m[row * sl.ld + j] != want) return NK_ECOMM;
+      }
+  }
   return NK_OK;
 }
 

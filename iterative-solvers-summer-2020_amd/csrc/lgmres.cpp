@@ -496,6 +496,8 @@ int NewtonKrylov::device_steps() {
       tl.t = t + 1;
       tl.nval = nval;
       tl.peer = !one;
+      static const uint64_t ticks = device_wait_ticks();
+      tl.wait_ticks = ticks;
       if (have_pa) tl.pa = pa;
     }
     bool tail_used = false;

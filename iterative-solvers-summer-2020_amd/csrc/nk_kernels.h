@@ -24,6 +24,9 @@ bool peer_fuse_enabled();
 // communicator (and NKHIP_PEER_FUSE on): NKHIP_SLAB_XK=2 when no two ranks share a GPU, 1
 // always (tests: several processes on one GPU); unset / 0: off (read per call).
 bool slab_x_enabled(const nk_comm* c);
+// wall_clock64() ticks of one bounded device-side wait: NKHIP_PEER_TIMEOUT_S seconds (default
+// 20) at the device's wall-clock rate (hipDeviceAttributeWallClockRate)
+uint64_t device_wait_ticks();
 
 // ---------------------------------------------------------------------------------------------
 struct Field {
@@ -195,6 +198,7 @@ struct ArnTail {
   int t = 0;
   int nval = 0;                   // 2 nv + 3
   bool peer = false;
+  uint64_t wait_ticks = 0;        // bound of the reducers' wait (device_wait_ticks)
   PeerArgs pa{};
 };
 struct ArnoldiArgs {

@@ -40,6 +40,7 @@
 #include "../../include/nkhip.h"
 #include "comm.h"
 #include "nk_device.h"
+#include "nk_kernels.h"
 #include "peer_dev.h"
 
 namespace nk {
@@ -127,8 +128,10 @@ uint64_t process_nonce() {
   return v;
 }
 
-// wall_clock64() ticks of one bounded wait: NKHIP_PEER_TIMEOUT_S seconds (default 20)
-uint64_t wait_ticks() {
+uint64_t wait_ticks() { return device_wait_ticks(); }
+}  // namespace
+
+uint64_t device_wait_ticks() {
   int dev = 0, khz = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
@@ -138,6 +141,8 @@ uint64_t wait_ticks() {
   if (!(s > 0)) s = 20.0;
   return uint64_t(s * 1e3 * double(khz));
 }
+
+namespace {
 
 struct PeerComm final : nk_comm {
   int r = 0, p = 1;

@@ -91,7 +91,7 @@ __device__ __forceinline__ uint64_t* xflag(char* b, int P, int64_t max_nx, int p
 __device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const char* me, int* err,
                                      uint64_t ticks) {
   const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(me + kOffAbort);
-  uint64_t t0 = 0;
+  const uint64_t t0 = wall_clock64();  // once: a wrapping poll count must not restart it
   for (uint32_t n = 0;; ++n) {
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag) {
       __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope
@@ -99,7 +99,6 @@ __device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const c
     }
     if ((n & 63) == 0) {
       const uint64_t now = wall_clock64();
-      if (n == 0) t0 = now;
       if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
           now - t0 > ticks) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

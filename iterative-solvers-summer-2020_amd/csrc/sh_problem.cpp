@@ -51,11 +51,19 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
     hu_ = h + 12 * nx;
     y4_ = h + 16 * nx;
     yh_ = h + 20 * nx;
-    // every rank must take the fused Arnoldi path or none: decide on the smallest and the
-    // largest slab (one all-reduce; every rank constructs its problem)
-    double mm[2] = {-double(ny), double(ny)};
+    // the halo slots of the pushed-halo-rows path (peer-memory communicator, one stepper)
+    if (!E_.comm->claim_slots(this, &slots_) || slots_.ld < nx) {
+      if (slots_.mine) E_.comm->release_slots(this);
+      slots_ = nk_halo_slots{};
+    }
+    // every rank must take the fused Arnoldi path or none, and the pushed halo rows or none:
+    // decide on the smallest and the largest slab and on whether any rank went without its
+    // slots (one all-reduce; every rank constructs its problem).  A rank whose slots another
+    // stepper still holds would otherwise read slots its neighbours never push, or wait in halo
+    // exchanges they never join.
+    double mm[3] = {-double(ny), double(ny), slots_.mine ? 0.0 : 1.0};
     if (hipMemcpyAsync(y4_, mm, sizeof(mm), hipMemcpyHostToDevice, E_.s) != hipSuccess ||
-        E_.comm->allreduce(y4_, 0, 2, E_.s) != NK_OK ||
+        E_.comm->allreduce(y4_, 0, 3, E_.s) != NK_OK ||
         hipMemcpyAsync(mm, y4_, sizeof(mm), hipMemcpyDeviceToHost, E_.s) != hipSuccess ||
         hipStreamSynchronize(E_.s) != hipSuccess) {
       status_ = NK_ECOMM;
@@ -63,8 +71,10 @@ SHProblem::SHProblem(Engine& E, int64_t ny, int64_t nx, int64_t ny_global, SHCoe
     }
     ny_min_ = int64_t(-mm[0]);
     ny_max_ = int64_t(mm[1]);
-    // the halo slots of the pushed-halo-rows path (peer-memory communicator, one stepper)
-    if (!E_.comm->claim_slots(this, &slots_) || slots_.ld < nx) slots_ = nk_halo_slots{};
+    if (mm[2] > 0.0 && slots_.mine) {  // some rank has none: no rank pushes
+      E_.comm->release_slots(this);
+      slots_ = nk_halo_slots{};
+    }
     if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming) != hipSuccess) {

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("nk_comm_destroy", C.c_int, [_P]),
     ("nk_comm_abort", C.c_int, [_P]),
     ("nk_comm_selftest", C.c_int, [_P, _I64, _P]),
+    ("nk_comm_selftest_push", C.c_int, [_P, _I64, _P]),
     ("nk_sh_create", C.c_int, [C.POINTER(_P), _I64, _I64, _I64, _D, _D, _D, _D,
                                C.POINTER(nk_opts), _P, _P]),
     ("nk_sh_destroy", C.c_int, [_P]),

@@ -62,6 +62,17 @@ class Comm:
         stream = torch.cuda.current_stream().cuda_stream
         return lib.nk_comm_selftest(self.handle, int(nx), C.c_void_p(stream)) == 0
 
+    def selftest_push(self, nx: int = 64):
+        """A collective: the pushed-halo-rows protocol of the slab solver (push into the
+        neighbours' halo slots, one all-reduce, read back, host check; nk_comm_selftest_push).
+        True / False (a row did not arrive intact or a wait gave up), or None when the group has
+        no halo slots to check (RCCL, or a stepper holds them) -- the same answer on every rank
+        except for False, which the caller must agree on over its side channel."""
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+        rc = lib.nk_comm_selftest_push(self.handle, int(nx), C.c_void_p(stream))
+        return None if rc == -1 else rc == 0
+
 
 class RcclComm(Comm):
     @staticmethod

@@ -31,6 +31,8 @@ def test_bench_self_launch_four_ranks_one_gpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 4 and d["steps"] == 2 and d["warmup"] == 1
     assert d["config"]["comm"] == "PeerComm", d["config"]
+    assert d["comm_check"] == {"selftest": "ok", "pushed_rows_selftest": "ok",
+                               "slab_path": "pushed"}, d["comm_check"]
     assert d["config"]["parallelism"] == "row-slab x4"
     fc = d["final_step_check"]
     assert fc["max_abs_residual"] <= fc["f_tol"], fc
@@ -40,3 +42,40 @@ def test_bench_self_launch_four_ranks_one_gpu():
     # the roofline names the dominant streaming kernel (with four ranks time-sharing one GPU the
     # slab edge kernel's waits for the other processes are the largest kernel time: excluded)
     assert d["value"] > 0 and d["roofline"]["kernel"] == "arnoldi_fused"
+
+
+@pytest.mark.timeout(600)
+def test_bench_push_selftest_fault_falls_back_and_config5_leg():
+    """Two things of the N > 1 line in one self-launched 2-rank run on this GPU:
+    * fault injection: rank 1 pushes wrong rows in the pushed-halo-rows self-test
+      (NKHIP_PEER_SELFTEST_BREAK_PUSH=1); every rank must then take the edge + halo exchange
+      path (comm_check records it, the slab A/B skips the pushed variants) and still produce a
+      root of the oracle residual;
+    * config 5's leg after the headline (other_configs.config5: the grid of
+      NKHIP_BENCH_CONFIG5_N, here 2048^2 instead of 16384^2, on the same ranks; its whole-grid
+      oracle residual within f_tol)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(NKHIP_BENCH_ONE_DEVICE="1", NKHIP_PEER_SELFTEST_BREAK_PUSH="1",
+               NKHIP_BENCH_CONFIG5_N="2048")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--n",
+                        "1024", "--steps", "1", "--warmup", "1", "--extra", "on", "--pmc", "off",
+                        "--probes", "off", "--slab-ab", "1"],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=540)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["comm_check"]["pushed_rows_selftest"] == "failed on some rank", d["comm_check"]
+    assert d["comm_check"]["slab_path"] == "edge_halo"
+    assert "pushed_ms_per_arnoldi" not in d["slab_exchange_ab"], d["slab_exchange_ab"]
+    assert d["slab_exchange_ab"]["edge_halo_ms_per_arnoldi"] > 0
+    fc = d["final_step_check"]
+    assert fc["max_abs_residual"] <= fc["f_tol"], fc
+    c5 = d["other_configs"]["config5"]
+    assert c5["grid"] == 2048 and c5["n_gpus"] == 2 and c5["steps_per_s"] > 0, c5
+    assert c5["ms_per_arnoldi_step"] > 0 and c5["newton_its_per_step"] >= 1
+    assert c5["final_step_residual"] <= c5["f_tol"], c5
+    assert c5["comm"] == "PeerComm"
+    assert c5["comm_check"]["slab_path"] == "edge_halo"  # the injected fault holds for its group

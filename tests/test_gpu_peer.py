@@ -100,7 +100,8 @@ def _free_port():
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,N,steps,xk,tail", [
     (2, 128, 2, "auto", None), (2, 61, 1, "auto", None), (3, 96, 1, "auto", None),
-    (4, 128, 1, "auto", None), (8, 256, 1, "auto", None), (2, 128, 2, "1", None),
+    (4, 128, 1, "auto", None), (8, 256, 1, "auto", None), (2, 200, 1, "auto", None),
+    (2, 200, 1, "1", None), (2, 128, 2, "1", None),
     (3, 96, 1, "1", None), (4, 256, 1, "1", None), (2, 128, 2, "auto", "2"),
     (4, 256, 1, "auto", "2")])
 def test_peer_processes_match_single_slab(world, N, steps, xk, tail, tmp_path):
@@ -113,7 +114,8 @@ def test_peer_processes_match_single_slab(world, N, steps, xk, tail, tmp_path):
     progresses -- publishing never waits -- but slowly; "auto" takes the edge + halo kernel).
     tail = "2": the fused launches' tails run the reduction, the all-reduce and the control
     although the ranks share this GPU (NKHIP_ARN_TAIL=2; by default they do so only with one
-    rank per GPU)."""
+    rank per GPU).  N = 200 on 2 ranks: 100-row slabs whose band plan ends in a one-row band, so
+    the band before it also reads the halo rows ny, ny+1 (it computes / waits for them itself)."""
     import subprocess
     U0 = np.random.default_rng(2020).standard_normal((N, N))
     import nkhip
@@ -212,13 +214,13 @@ comm.close()
 """
 
 
-def test_peer_world1_push_matches_exchange_bitwise(monkeypatch):
+@pytest.mark.parametrize("N", [128, 100])
+def test_peer_world1_push_matches_exchange_bitwise(N, monkeypatch):
     """The pushed-halo-rows path (default: every producer writes its edge rows into the
     neighbours' halo slots, the fused kernel's edge bands form u on the halo rows from them) and
     the edge + halo exchange kernel (NKHIP_SLAB_PUSH=0) give the same bits: the halo rows are
-    the same update sums in the same order."""
+    the same update sums in the same order.  N = 100: a band plan ending in a one-row band."""
     import nkhip
-    N = 128
     U0 = np.random.default_rng(7).standard_normal((N, N))
     out = {}
     for mode in ("1", "0"):
@@ -320,3 +322,42 @@ def test_config5_16384_eight_processes(tmp_path):
     torch.cuda.empty_cache()
     assert abs(nit1 - nits.pop()) <= 1
     assert float(np.abs(U1 - Us).max()) <= 1e-5 * max(1.0, float(np.abs(Us).max()))
+
+
+_PUSH_WORKER = r"""
+import os, sys
+import torch
+import torch.distributed as dist
+sys.path[:0] = [{root!r}, {pkg!r}]
+import nkhip
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+NX = int(os.environ["WIDE_NX"])
+comm = nkhip.PeerComm.from_torch_distributed(max_nx=NX)
+res = [comm.selftest_push(NX) for _ in range(2)]
+_, ny = nkhip.slab_rows(64, int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]))
+m = nkhip.SwiftHohenberg(N=64, d=40.0, comm=comm, ny_local=ny)
+held = comm.selftest_push(NX)  # the stepper holds the slots: nothing to check, on every rank
+m.close()
+after = comm.selftest_push(NX)
+torch.cuda.synchronize()
+dist.barrier()
+comm.close()
+print(f"push {{res}} held {{held}} after {{after}}", flush=True)
+"""
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("world,brk", [(1, None), (3, None), (2, "1")])
+def test_peer_push_selftest(world, brk, tmp_path):
+    """nk_comm_selftest_push -- the pushed-halo-rows protocol as the solver runs it (push into
+    the neighbours' slots, no flag, one all-reduce, read back in a kernel, host check): passes on
+    1 and 3 processes; with rank 1 pushing wrong rows (NKHIP_PEER_SELFTEST_BREAK_PUSH=1) its
+    neighbour (rank 0) fails it; while a stepper holds the slots it is skipped on every rank."""
+    env = {"WIDE_NX": "4096"}
+    if brk is not None:
+        env["NKHIP_PEER_SELFTEST_BREAK_PUSH"] = brk
+    outs = _run_workers(tmp_path, _PUSH_WORKER, world, env, timeout=150)
+    for r, o in enumerate(outs):
+        want = "[False, False]" if (brk is not None and r == 0) else "[True, True]"
+        assert f"push {want} held None after" in o, (r, o)
