@@ -243,7 +243,7 @@ def config2_lap5(n=1024, reps=200, rocprof=True):
     return {"workload": f"lap5_{n}x{n}_fp64", "avg_us_per_launch_incl_gap": round(us, 2),
             "alg_GBps": round(16 * n * n / (us * 1e-6) / 1e9, 1), "max_abs_err_vs_oracle": err,
             "cpu_scipy_csr_ms": round(best * 1e3, 3),
-            "roofline": {"kernel": "march_kernel<LAP5>", "bound": "hbm",
+            "roofline": {"kernel": "tile_kernel<LAP5>", "bound": "hbm",
                          "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4), "avg_us": round(k_us, 2),
                          "alg_bytes_per_launch": 16 * n * n,
@@ -253,8 +253,9 @@ def config2_lap5(n=1024, reps=200, rocprof=True):
                                              "HIP event pair around each launch"),
                          "event_pair_us": round(ev_us, 2),
                          "mall_resident": True,
-                         "note": "the 16.8 MB working set (v, y) stays in the 256 MB Infinity "
-                                 "Cache between launches, so HBM is not what bounds it"},
+                         "note": "the 16.8 MB working set (v, y) stays on chip between "
+                                 "launches (each XCD's 2 MB slice in its 4 MB L2, the rest in "
+                                 "the 256 MB Infinity Cache), so HBM is not what bounds it"},
             "note": "back-to-back launches; rocprofv3 durations in profiles/r02_config2.md"}
 
 
@@ -283,7 +284,7 @@ def config2_rocprof():
             for f in files:
                 if f.endswith("kernel_stats.csv"):
                     for row in csv.DictReader(open(os.path.join(root, f))):
-                        if "march_kernel" in row["Name"]:
+                        if "tile_kernel" in row["Name"] or "march_kernel" in row["Name"]:
                             return {"avg_us": float(row["AverageNs"]) / 1e3,
                                     "calls": int(row["Calls"])}
         return None
@@ -481,17 +482,21 @@ def jvp_isolated(n, h, r, k, g, x0, jvp, reps=20):
             "source": f"{reps} back-to-back launches on resident {n}^2 inputs after the timed region"}
 
 
-def copy_bandwidth(n, reps=20):
+def copy_bandwidth(n, reps=20, scale=4):
     """This box's streaming rate, measured after the timed region so roofline fractions can be
-    compared across boxes (their HBM spread is ~15 %): n^2 fp64 device-to-device copies (read one
-    vector, write one: 16 B/pt) by nk_stream_copy (16-KB chunks per block, non-temporal; the
-    guide's float4-copy pattern, ~6.3 TB/s) and, for reference, torch's copy_; alternating between
-    two buffer pairs so the 4 x n^2 working set (537 MB at 4096^2) exceeds the 256 MB Infinity
-    Cache; HIP events on the current stream.  peak_measured = the faster of the two."""
+    compared across boxes (their HBM spread is ~15 %): fp64 device-to-device copies of scale x n^2
+    elements (read one vector, write one: 16 B/pt) by nk_stream_copy (16-KB chunks per block,
+    non-temporal; the guide's float4-copy pattern, ~6.3 TB/s) and, for reference, torch's copy_;
+    alternating between two buffer pairs so the working set (2.1 GB at 4096^2) exceeds the 256 MB
+    Infinity Cache; HIP events on the current stream around back-to-back launches.  Copies of
+    4 x 4096^2 (~175 us each) keep the launch gaps to ~1 % of the time (round 5,
+    scripts/micro/copy_bench.hip: 1 x 4096^2 copies, ~44 us, lose ~3 % to them).
+    peak_measured = the faster of the two."""
     import torch
 
     import nkhip
-    bufs = [torch.empty(n * n, dtype=torch.float64, device="cuda") for _ in range(4)]
+    n2 = n * n * scale
+    bufs = [torch.empty(n2, dtype=torch.float64, device="cuda") for _ in range(4)]
     for b_ in bufs:
         b_.normal_()
 
@@ -506,15 +511,15 @@ def copy_bandwidth(n, reps=20):
         b.record()
         torch.cuda.synchronize()
         us = a.elapsed_time(b) * 1e3 / reps
-        return round(16.0 * n * n / (us * 1e-6) / 1e9, 1), round(us, 2)
+        return round(16.0 * n2 / (us * 1e-6) / 1e9, 1), round(us, 2)
 
     lib_gbs, lib_us = rate(lambda s_, d_: nkhip.stream_copy(s_, out=d_))
     torch_gbs, _ = rate(lambda s_, d_: d_.copy_(s_))
     del bufs
     return {"GB/s": max(lib_gbs, torch_gbs), "nk_stream_copy_GB/s": lib_gbs,
             "nk_stream_copy_avg_us": lib_us, "torch_copy_GB/s": torch_gbs,
-            "what": f"{n}^2 fp64 copies (16 B/pt), {reps} reps over two buffer pairs, HIP events, "
-                    "after the timed region"}
+            "what": f"{scale} x {n}^2 fp64 copies (16 B/pt), {reps} reps over two buffer pairs, "
+                    "HIP events around the back-to-back launches, after the timed region"}
 
 
 def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cpu", allow_rccl=True):
@@ -722,8 +727,9 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pus
     rows before the fused pass; in_kernel (NKHIP_SLAB_XK=2, =1 when the ranks share a GPU): the
     fused pass's edge bands exchange them themselves; pushed_tail (NKHIP_ARN_TAIL=1): pushed,
     with each step's reduction + all-reduce + control in the fused launch's last blocks (one rank
-    per GPU only: with ranks sharing a GPU it is the pushed path).  Returns (record, a, b), the
-    trajectory advanced."""
+    per GPU only: with ranks sharing a GPU it is the pushed path; its waits bounded by 3 s,
+    NKHIP_ARN_TAIL_TIMEOUT_S, so a stall fails the variant within seconds).  Returns (record, a,
+    b), the trajectory advanced."""
     names = ("pushed", "edge_halo", "in_kernel", "pushed_tail")
     if not pushed_ok:  # the pushed-halo-rows self-test failed (or there are no slots)
         names = ("edge_halo", "in_kernel")
@@ -731,13 +737,17 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pus
            "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
            "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2",
                          "NKHIP_ARN_TAIL": "0"},
-           "pushed_tail": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "1"}}
-    old = {k_: os.environ.get(k_) for k_ in ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK", "NKHIP_ARN_TAIL")}
+           "pushed_tail": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "1",
+                           "NKHIP_ARN_TAIL_TIMEOUT_S": "3"}}
+    keys = ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK", "NKHIP_ARN_TAIL", "NKHIP_ARN_TAIL_TIMEOUT_S")
+    old = {k_: os.environ.get(k_) for k_ in keys}
     acc = {n_: [0.0, 0] for n_ in names}
     failed = None
     try:
         for i in range(len(names) * rounds):
             name = names[i % len(names)]
+            for k_ in keys:
+                os.environ.pop(k_, None)
             os.environ.update(env[name])
             dist.barrier()
             torch.cuda.synchronize()

@@ -183,6 +183,12 @@ int nk_stream_copy(const double* src_dev, double* dst_dev, int64_t n, void* stre
  * line among them (0: none); reset != 0 clears the counters.  Synchronises the device.
  * NK_EINVAL from the product library (no checks compiled in). */
 int nk_debug_bounds(int64_t* violations, int32_t* first_line, int32_t reset);
+/* The fused kernel's block-halo mailbox, counted by the statistics build
+ * (`make mbstat`, nkhip/libnkhip_mbstat.so) since the last reset: counts[0] halo pairs the
+ * consumer lanes needed, [1] records not there at the first look, [2] extra polls, [3] pairs
+ * recomputed after kMBSpin polls.  NK_EINVAL from the other builds.  Diagnostic only: no
+ * reference interface. */
+int nk_debug_mailbox(int64_t* counts, int32_t reset);
 
 /* ---------------- communicators (row-slab decomposition over RCCL / xGMI) ---------------- */
 int nk_comm_unique_id_bytes(void);

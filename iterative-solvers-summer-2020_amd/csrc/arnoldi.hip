@@ -73,6 +73,14 @@ __device__ __forceinline__ double gld(const double* p) { return *(gdouble*)p; }
 // Stores through a raw buffer resource: a lane whose offset is out of range (kOOB) writes
 // nothing, so masked stores need no branch.
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
+// Cache policy of the fused kernels' streamed outputs (v, w' and their edge arrays): 0 = plain
+// (the line stays dirty in the XCD's L2 until evicted or the kernel-end release writes it back),
+// 16 = sc1 (written through and dropped from L2: no dirty L2 to write back at the kernel boundary;
+// MI355X_MICROARCH.md "stores of each flavour").  Build-time (ARN_OUT_POL) for the A/B.
+#ifndef ARN_OUT_POL
+#define ARN_OUT_POL 0
+#endif
+constexpr int kOutPol = ARN_OUT_POL;
 
 // Bounds-checked build (`make check` -> nkhip/libnkhip_check.so, -DNKHIP_ARN_CHECK; GPU
 // AddressSanitizer is not available on this pool).  Every index the fused kernels compute --
@@ -216,8 +224,15 @@ __device__ __forceinline__ dv2 gld2(const double* a) {
 // in time, profiles/r02_arnoldi_ab.md)
 constexpr uint32_t kMBCoh = 16;
 constexpr int kMBSpin = 2048;     // polls before a lane recomputes a missing halo pair itself
-__device__ __forceinline__ uint32_t mb_off(int64_t blk, int64_t T, int64_t t, int side, int comp) {
-  return uint32_t((((blk * T + t) * 4) + side * 2 + comp) * 16);
+#ifdef NKHIP_ARN_MBSTAT  // diagnostic build (`make mbstat`): what the mailbox consumers did
+// [0] halo pairs needed, [1] not there at the first look, [2] extra polls, [3] recomputed
+__device__ unsigned long long g_mb_stat[4];
+#define MB_STAT(i, v) atomicAdd(&g_mb_stat[i], static_cast<unsigned long long>(v))
+#else
+#define MB_STAT(i, v) ((void)0)
+#endif
+__device__ __forceinline__ uint32_t mb_off(uint32_t blk, uint32_t T, uint32_t t, int side, int comp) {
+  return (((blk * T + t) * 4) + uint32_t(side * 2 + comp)) * 16u;  // < mb_cap * 8 < 2^32
 }
 __device__ __forceinline__ bool mb_tag_ok(const u32x4& a, uint64_t tag) {
   return a.z == uint32_t(tag) && a.w == uint32_t(tag >> 32);
@@ -433,6 +448,24 @@ __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int
   *reinterpret_cast<dv2*>(d + col) = val;
 }
 
+// 32-bit row / column indices of the pair kernel's row loop, and a uniform value the compiler
+// must keep (an SGPR, or a VGPR lane when it spills) instead of re-reading it from the kernel
+// arguments
+typedef int ix_t;
+__device__ __forceinline__ int opaque_s(int x) {
+  x = __builtin_amdgcn_readfirstlane(x);
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ double opaque_d(double x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ const double* opaque_p(const double* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
 //   [V_0 .. V_{NV-1}, w, x0, (z)]
@@ -476,6 +509,10 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 #ifdef ARN_TAIL_PROBE  // timing build (scripts/dbg/tail_probe.py): stage times of the tails
 __device__ unsigned long long g_tail_probe[8];  // [0] tails, [1..5] summed stage ticks
 __device__ unsigned long long g_tail_first;     // wall clock of the current launch's first arrival
+// a tail that gave up: [0] 1 = its own blocks' arrival, 2 = the peer all-reduce; [1] blocks
+// arrived / [2] of total when it gave up; [3] bit q = peer q's contribution missing; [4] ticks
+// from the launch's first arrival to the give-up; [5] tails that gave up
+__device__ unsigned long long g_tail_diag[8];
 #endif
 constexpr int kTailR = 8;
 constexpr int kTailC = (2 * kArnMaxNV + 3 + kTailR - 1) / kTailR;  // values per reducer
@@ -512,6 +549,15 @@ __device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArn
   }
   __syncthreads();
   if (!ok) {  // a fault, not a path of this protocol: halt the queued launches and report it
+#ifdef ARN_TAIL_PROBE
+    if (threadIdx.x == 0) {
+      g_tail_diag[0] = 1;
+      g_tail_diag[1] = __hip_atomic_load(&T.S->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g_tail_diag[2] = total;
+      g_tail_diag[4] = wall_clock64() - g_tail_first;
+      atomicAdd(&g_tail_diag[5], 1ull);
+    }
+#endif
     if (threadIdx.x == 0) {
       st_sc1(T.prm + kArnMaxNV + 3, 1.0);
       if (T.peer && T.pa.err)
@@ -576,6 +622,20 @@ __device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArn
 #endif
   if (T.peer) {
     if (!peer_allreduce_wave(T.pa, redl, T.nval, T.nval)) {
+#ifdef ARN_TAIL_PROBE
+      {  // which peers' contributions never came (their flags in my buffer)
+        const int par = int(T.pa.tag & 1);
+        for (int q = lane; q < T.pa.P; q += 64)
+          if (__hip_atomic_load(red_flag(T.pa.base[T.pa.rank], par, q), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM) != T.pa.tag)
+            atomicOr(&g_tail_diag[3], 1ull << q);
+        if (lane == 0) {
+          g_tail_diag[0] = 2;
+          g_tail_diag[4] = wall_clock64() - g_tail_first;
+          atomicAdd(&g_tail_diag[5], 1ull);
+        }
+      }
+#endif
       if (lane == 0) T.prm[kArnMaxNV + 3] = 1.0;  // the queued fused step does nothing
       return;
     }
@@ -625,27 +685,39 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware mapping: consecutive blocks go round-robin over the 8 XCDs; give each XCD one
   // contiguous run of blocks (whole bands), so band halos are shared inside one L2.
-  const int64_t b = blockIdx.x;
-  const int64_t bpx = gridDim.x / 8;  // grid is a multiple of 8
-  const int64_t L = (b % 8) * bpx + b / 8;
-  const int64_t ngroups = (A.strips + WB - 1) / WB;  // a block = WB adjacent strips
+  const ix_t b = blockIdx.x;
+  const ix_t bpx = gridDim.x / 8;  // grid is a multiple of 8
+  const ix_t L = (b % 8) * bpx + b / 8;
+  const ix_t ngroups = (A.strips + WB - 1) / WB;  // a block = WB adjacent strips
   if (L >= ngroups * A.nbands) return;                 // whole blocks only
-  const int64_t band = L / ngroups, grp = L % ngroups;
-  const int64_t gw = L * WB + wid;  // partial-sum column of this wave
-  const int64_t nx = A.nx, ny = A.ny;
-  const int64_t B0 = grp * WB * kSW;        // the block's first column
-  const int64_t c = B0 + wid * kSW + 2 * l;  // columns past nx compute wrapped columns, masked
-  const int64_t col = c % nx;                // nx even: c and c+1 wrap together
+  const ix_t band = L / ngroups, grp = L % ngroups;
+  const ix_t gw = L * WB + wid;  // partial-sum column of this wave
+  // row and column arithmetic in 32 bits (ny * nx * 8 < 2^32, arnoldi_supported), the grid
+  // scalars opaque: the compiler keeps them in registers instead of reloading them from the
+  // kernel arguments inside the row loop (every such reload is a scalar load whose lgkmcnt wait
+  // also drains the wave's LDS queue; ~20 per row at nv 19-24 before)
+  const ix_t nx = opaque_s(ix_t(A.nx)), ny = opaque_s(ix_t(A.ny));
+  const ix_t B0 = grp * WB * kSW;        // the block's first column
+  const ix_t c = B0 + wid * kSW + 2 * l;  // columns past nx compute wrapped columns, masked
+  const ix_t col = c % nx;                // nx even: c and c+1 wrap together
   const bool own = c < nx;
   // block halo: h = 0, 1 -> columns B0-2, B0-1; h = 2, 3 -> B0 + WB*64, +1
   const int hh = lane & 3;
-  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WB * kSW - 2 + hh;
-  const int64_t hcol = ((hc % nx) + nx) % nx;
-  const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
-  const int64_t r0 = A.r_begin + band * A.RY;
-  const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
-  const int64_t nrows = r1 - r0;
-  const SHCoef& K = A.k;
+  const ix_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WB * kSW - 2 + hh;
+  const ix_t hcol = ((hc % nx) + nx) % nx;
+  const ix_t rend = (A.r_end >= 0) ? ix_t(A.r_end) : ny;
+  const ix_t r0 = opaque_s(ix_t(A.r_begin) + band * A.RY);
+  const ix_t r1 = opaque_s((r0 + A.RY < rend) ? r0 + A.RY : rend);
+  const ix_t nrows = r1 - r0;
+  // the stencil coefficients in registers for the whole loop (re-read from the kernel
+  // arguments per row otherwise: a scalar load and an lgkmcnt wait each)
+  SHCoef K = A.k;
+  K.c0 = opaque_d(K.c0);
+  K.c1 = opaque_d(K.c1);
+  K.c2 = opaque_d(K.c2);
+  K.c3 = opaque_d(K.c3);
+  K.g = opaque_d(K.g);
+  K.ik = opaque_d(K.ik);
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
@@ -697,35 +769,36 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     for (int j = 0; j < NV; ++j) p = (e == j) ? A.E[j] : p;
     hE = p;
   }
-  const int64_t grpR = (grp + 1 < ngroups) ? grp + 1 : 0;
+  const ix_t grpR = (grp + 1 < ngroups) ? grp + 1 : 0;
   // edge-array stores of the outputs: the lane holding columns B, B+1 of a boundary B writes
   // them as E[b][q][2..3]; the lane holding B-2, B-1 as E[b][q][0..1] (b = 0 for nx - 2, nx - 1)
-  const int64_t nbE = edge_groups(nx);  // (the 2-wave mailbox blocks are narrower than a group)
-  const int64_t nelem = ny * nx, eelem = edge_elems(ny, nx);
+  const ix_t nbE = edge_groups(nx);  // (the 2-wave mailbox blocks are narrower than a group)
+  const ix_t nelem = ny * nx, eelem = edge_elems(ny, nx);
   const bool eL = own && (c % kEdgeW == 0);
   const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
-  const int64_t ebo = eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
+  const ix_t ebo = eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
   const bool eOn = eL || eR;
   const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
   const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
   // byte offset of this lane's edge pair at row q (kOOB: nothing to store)
-  auto eoff = [&](int64_t q) -> uint32_t {
+  auto eoff = [&](ix_t q) -> uint32_t {
     return eOn ? uint32_t(CI((ebo / 4) * ny * 4 + q * 4 + (ebo & 3), eelem - 1) * 8) : kOOB;
   };
-  const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
+  const double* x0p = opaque_p(A.x0);  // (kept in registers, as the grid scalars above)
+  const double* hxp = (EXT && lane >= 4) ? A.z : x0p;  // lanes 0-3: x0 halo, 4-7: z halo
   // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their u arrives in A.yh (the x0 entry
   // and the x0 halo lanes read it there in place of x0)
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
-  const int64_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
+  const ix_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
 
-  auto wrap = [&](int64_t q) -> int64_t {
+  auto wrap = [&](ix_t q) -> ix_t {
     q = (q > r1 + 1) ? r1 + 1 : q;  // past the band halo: re-read its last row
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
   // a neighbour slab's halo row (u taken from A.yh)
-  auto halo_row = [&](int64_t q) -> bool {
-    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
+  auto halo_row = [&](ix_t q) -> bool {
+    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
     return slab && (qc < 0 || qc >= ny);
   };
 
@@ -733,19 +806,19 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   // need its left halo pair, wave WB-1's lanes l == 31 its last pair and the right halo pair
   constexpr int BW = WB * kSW;
   constexpr bool mb = MB && !EXT;  // a separate instantiation: the plain one has none of it
-  const int64_t mbT = A.RY + 8;             // records per block and side (rows pushed <= RY + 7)
+  const ix_t mbT = A.RY + 8;             // records per block and side (rows pushed <= RY + 7)
   const __amdgpu_buffer_rsrc_t rmb = rsrc(A.mb, mb ? A.mb_cap : 0);
   const uint64_t tag = A.mb_tag;
   const bool needL = mb && wid == 0 && l == 0, needR = mb && wid == WB - 1 && l == 31;
-  const int64_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
+  const ix_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
   const int nside = needL ? 1 : 0;  // my left halo = the left neighbour's right-edge records
   const bool prod = mb && ((wid == 0 && lane == 0) || (wid == WB - 1 && lane == 31));
   const int pside = (wid == 0 && lane == 0) ? 0 : 1;
-  const int64_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;  // the halo pair's columns
+  const ix_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;  // the halo pair's columns
   // this lane stopped polling (a neighbour was not there in time; mb_recompute: test switch)
   bool mb_dead = A.mb_recompute;
-  auto mb_need = [&](int64_t q) -> bool { return (needL || needR) && !halo_row(q); };
-  auto poll = [&](int64_t q, u32x4* a, u32x4* b) {  // issue the two record loads of row q
+  auto mb_need = [&](ix_t q) -> bool { return (needL || needR) && !halo_row(q); };
+  auto poll = [&](ix_t q, u32x4* a, u32x4* b) {  // issue the two record loads of row q
     const bool on = mb_need(q) && !mb_dead;
     const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
     ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
@@ -758,8 +831,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     return e < NV ? A.V[e] : (e == NV ? A.w : ((e == EX || !EXT) ? A.x0 : A.z));
   };
   auto cfd = [&](int e) -> double { return e < NV ? arn_c(A, e) : (e == NV ? a_tau : 0.0); };
-  auto recompute = [&](int64_t q) -> dv2 {
-    const int64_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
+  auto recompute = [&](ix_t q) -> dv2 {
+    const ix_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
     double p0x = 0.0, p0y = 0.0, p1x = 0.0, p1y = 0.0;
 #pragma unroll 1
     for (int k = 0; k < NI; ++k) {
@@ -775,21 +848,26 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     return dv2{p0x + p1x, p0y + p1y};
   };
   // the halo pair of row q (-0.0 where the lane needs none: adding it changes nothing)
-  auto mb_halo = [&](int64_t q, u32x4 a, u32x4 b) -> dv2 {
+  auto mb_halo = [&](ix_t q, u32x4 a, u32x4 b) -> dv2 {
     const bool need = mb_need(q);
     bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
+    if (need) MB_STAT(0, 1);
     dv2 h{mb_val(a), mb_val(b)};
     if (!ok) {  // the neighbour is behind (or was not there): poll, then recompute
+      MB_STAT(1, 1);
       const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
-      for (int n = 0; n < kMBSpin && !mb_dead && !ok; ++n) {
+      int n = 0;
+      for (; n < kMBSpin && !mb_dead && !ok; ++n) {
         __builtin_amdgcn_s_sleep(2);
         a = __builtin_amdgcn_raw_buffer_load_b128(rmb, o, 0, kMBCoh);
         b = __builtin_amdgcn_raw_buffer_load_b128(rmb, o + 16, 0, kMBCoh);
         ok = mb_tag_ok(a, tag) && mb_tag_ok(b, tag);
       }
+      MB_STAT(2, n);
       if (ok) {
         h = dv2{mb_val(a), mb_val(b)};
       } else {
+        MB_STAT(3, 1);
         mb_dead = true;
         h = recompute(q);
       }
@@ -803,30 +881,30 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     double hx;
     bool own;  // row of this slab (false: a neighbour's halo row, u taken from A.yh)
   };
-  auto load = [&](Slot& s, int64_t q) {
-    const int64_t qq = wrap(q);
-    const int64_t o = CI(qq * nx + col, nelem - 1);
-    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
+  auto load = [&](Slot& s, ix_t q) {
+    const ix_t qq = wrap(q);
+    const ix_t o = CI(qq * nx + col, nelem - 1);
+    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
     const bool hrow = halo_row(q);
-    const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
-    const int64_t yo = CI(hq * yld + col, 4 * yld - 1);
+    const ix_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
+    const ix_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const double* a = ep[k] + o;
       if (k == EX / 2) a = (hrow && hf == (EX & 1)) ? yhb + yo : a;
       s.e[k] = gld2<NT>(a);
     }
-    const int64_t ho = CI(qq * nx + hcol, nelem);
+    const ix_t ho = CI(qq * nx + hcol, nelem);
     // block halo: from the entry's edge array (four rows per line) or from the vector itself;
     // with the mailbox a load of one fixed line (keeps the row's load batch the same shape)
     if constexpr (!EXT && !mb) {
-      const int64_t eo = CI(useE ? ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh : 0, eelem);
+      const ix_t eo = CI(useE ? ((((hh < 2) ? grp : grpR) * ny + qq) << 2) + hh : 0, eelem);
       s.hv = gld(useE ? hE + eo : hp + ho);
     }
     // z on the halo columns (EXT, lanes 4..); u of a slab halo row (A.yh, lanes 0-3); every
     // other lane one fixed line of x0 (not of A.yh: the halo rows may sit in uncached peer memory)
-    const int64_t hyo = CI(hq * yld + hcol, 4 * yld);
-    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? A.x0 : hxp + ho));
+    const ix_t hyo = CI(hq * yld + hcol, 4 * yld);
+    s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? x0p : hxp + ho));
     s.own = !hrow;
   };
   // entry e of this row for both halves (e is a compile-time index)
@@ -839,7 +917,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     return dv2{mine ? x.x : px, mine ? x.y : py};
   };
   // the basis entries and x0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
-  auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
+  auto stash = [&](const Slot& s, const dv2& g, ix_t q) {
     dv2 (*d)[64] = lg[(q - r0) & 1];
 #pragma unroll
     for (int k = 0; k < NB; ++k) d[k][lane] = s.e[k];
@@ -851,7 +929,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
 #pragma unroll
   for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
   dv2 gq{0.0, 0.0};  // x0 of the last pushed row (both halves)
-  auto push = [&](const Slot& s, int64_t q) {
+  auto push = [&](const Slot& s, ix_t q) {
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {  // explicit FMAs: the mailbox's recompute() repeats them
@@ -944,11 +1022,11 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const bool st = own && hf == 0 && q >= r0 && q < r1;
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
-                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
+                                           CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)  // wave-uniform
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
-                                             st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
+                                             st ? eoff(q) : kOOB, 0, kOutPol);  // (eoff checks)
     return dv2{cm2 + cp2, cm1 + cp3};  // h2 of row q
   };
 
@@ -965,7 +1043,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   //   (a/sc) [u/k - (L u + u (g (2 x0 + t) - (3 x0 (x0 + t) + t^2)))/2],  t = a u,
   // without the cancellation of two G evaluations (and without reading G0).
   const double zs = a_alpha * isc;
-  auto centre = [&](int64_t r) {
+  auto centre = [&](ix_t r) {
     const dv2 (*d)[64] = lg[(r - r0) & 1];
     const dv2 x0r = d[NB][lane];
     dv2 wo;
@@ -983,12 +1061,11 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           CO((in && hf == 0) ? uint32_t((r * nx + col) * 8) : kOOB, nelem),
-                                           0, 0);
+                                           CO((in && hf == 0) ? uint32_t(r * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in && hf == 0, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
-                                             (in && hf == 0) ? eoff(r) : kOOB, 0, 0);
+                                             (in && hf == 0) ? eoff(r) : kOOB, 0, kOutPol);
     const dv2 wm = in ? wo : dv2{0.0, 0.0};
     const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
 #pragma unroll
@@ -1003,7 +1080,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     avv = __builtin_fma(vh.y, vm.y, __builtin_fma(vh.x, vm.x, avv));
     aww = __builtin_fma(wh.y, wm.y, __builtin_fma(wh.x, wm.x, aww));
   };
-  auto push_h2 = [&](const Slot& s, int64_t q) {
+  auto push_h2 = [&](const Slot& s, ix_t q) {
     const dv2 h2 = push(s, q);
     h2w[0] = h2w[1];
     h2w[1] = h2w[2];
@@ -1057,10 +1134,10 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       // whole groups of RR rows with no branch inside the group (a branch would make the
       // compiler's wait-count analysis drain every load in flight): rows past the band end
       // are computed on clamped rows and masked out of the stores and sums
-      for (int64_t t0 = 0; t0 < nrows; t0 += RR) {
+      for (ix_t t0 = 0; t0 < nrows; t0 += RR) {
 #pragma unroll
         for (int k = 0; k < RR; ++k) {
-          const int64_t r = r0 + t0 + k;
+          const ix_t r = r0 + t0 + k;
           u32x4 ma, mb2;
           if constexpr (mb) poll(r + 1, &ma, &mb2);  // before the row's batch: its wait
                                                      // leaves the batch in flight
@@ -1388,11 +1465,11 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     vw[4] = v;
     const bool st = own && q >= r0 && q < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
-                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, 0);
+                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
-                                             st ? eoff(q) : kOOB, 0, 0);  // (eoff checks)
+                                             st ? eoff(q) : kOOB, 0, kOutPol);  // (eoff checks)
     return dv2{cm2 + cp2, cm1 + cp3};
   };
 
@@ -1423,11 +1500,11 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           CO(in ? uint32_t((r * nx + col) * 8) : kOOB, nelem), 0, 0);
+                                           CO(in ? uint32_t((r * nx + col) * 8) : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
-                                             in ? eoff(r) : kOOB, 0, 0);
+                                             in ? eoff(r) : kOOB, 0, kOutPol);
     const dv2 wm = in ? wo : dv2{0.0, 0.0};
     const dv2 vm = in ? vw[2] : dv2{0.0, 0.0};
 #pragma unroll
@@ -1803,6 +1880,12 @@ extern "C" int nk_debug_tail_probe(unsigned long long* out) {
   static const unsigned long long zero[8] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
+// g_tail_diag (a tail that gave up), read without synchronising the device (it may be the one
+// whose stream failed)
+extern "C" int nk_debug_tail_diag(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_diag), sizeof(g_tail_diag)) == hipSuccess ? 0
+                                                                                             : -1;
+}
 #endif
 
 bool arnoldi_wide(int nv) {
@@ -1824,6 +1907,27 @@ hipError_t arnoldi_launch(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) 
   if (!al) return hipErrorInvalidValue;  // 16-B loads and stores
   if (A.z) return launch_e<true>(A, s, nwaves);
   return launch_e<false>(A, s, nwaves);
+}
+
+int arnoldi_mailbox_counters(int64_t out[4], bool reset) {
+#ifdef NKHIP_ARN_MBSTAT
+  unsigned long long c[4];
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(c, HIP_SYMBOL(g_mb_stat), sizeof(c), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -2;
+  for (int i = 0; i < 4; ++i) out[i] = int64_t(c[i]);
+  if (reset) {
+    for (int i = 0; i < 4; ++i) c[i] = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_mb_stat), c, sizeof(c), 0, hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return -2;
+  }
+  return 0;
+#else
+  (void)out;
+  (void)reset;
+  return -1;  // not the mailbox-statistics build
+#endif
 }
 
 int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset) {

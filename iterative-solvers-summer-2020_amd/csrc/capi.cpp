@@ -367,6 +367,12 @@ int nk_debug_bounds(int64_t* violations, int32_t* first_line, int32_t reset) {
   return rc == 0 ? NK_OK : (rc == -1 ? NK_EINVAL : NK_EHIP);
 }
 
+int nk_debug_mailbox(int64_t* counts, int32_t reset) {
+  if (!counts) return NK_EINVAL;
+  const int rc = arnoldi_mailbox_counters(counts, reset != 0);
+  return rc == 0 ? NK_OK : (rc == -1 ? NK_EINVAL : NK_EHIP);
+}
+
 // ------------------------------------------------------------------------------ comms
 int nk_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
 int nk_comm_get_unique_id(void* out) { return out ? comm_get_unique_id(out) : NK_EINVAL; }

@@ -24,6 +24,7 @@
 // launches and the host only queues launches ahead of it; the kernel hands the step that ends
 // the process (or that needs a path it does not take) back to this loop.  NKHIP_DEVCTL=1/0
 // forces it on/off (default: on with a communicator, see devctl_enabled).
+#include <algorithm>
 #include <atomic>
 #include <cstddef>
 #include <cfloat>
@@ -60,13 +61,17 @@ bool lag_enabled() {
 }
 }  // namespace
 
-int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bool dev_scale) {
+int NewtonKrylov::issue_step(int j, const double* z, double zs, double znorm, bool dev_scale,
+                             bool have_w) {
   const int64_t n = E_.n;
   zp_[j] = z;
   hS_->zs[j] = zs;  // provisional when the exact scale of z is only known later
   double* w = V_[j + 1];
   int rc;
-  if (dev_scale) {  // z = raw basis vector whose |z|^2 the combo left in device memory
+  if (have_w) {  // the speculative JVP of the line search computed it (NewtonKrylov::line_search)
+    rc = NK_OK;
+    st_->njvp += 1;
+  } else if (dev_scale) {  // z = raw basis vector whose |z|^2 the combo left in device memory
     rc = P_.jvp_dev(X_, G0_, z, E_.dres(Engine::kSlotCombo), omega_, w);
     st_->njvp += 1;
   } else if (znorm == 0.0) {  // KrylovJacobian.matvec: a zero vector maps to zero, no F call
@@ -174,7 +179,11 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     const double* z;
     double zs, zn;
     input(0, &z, &zs, &zn);
-    rc = issue_step(0, z, zs, zn, false);
+    // the line search's speculative JVP applied J to this same input at this same point
+    const bool have = spec_.valid && n_o > 0 && z == spec_.z && zs == spec_.zs &&
+                      zn == spec_.zn && V_[1] == spec_.w;
+    spec_.valid = false;
+    rc = issue_step(0, z, zs, zn, false, have);
   }
   sig_est[0] = 0.0;
   if (!rc) rc = E_.sync();
@@ -499,6 +508,17 @@ int NewtonKrylov::device_steps() {
       static const uint64_t ticks = device_wait_ticks();
       tl.wait_ticks = ticks;
       if (have_pa) tl.pa = pa;
+      // NKHIP_ARN_TAIL_TIMEOUT_S (read per launch): a shorter bound for the tail's waits -- its
+      // own blocks' arrival and the peer all-reduce inside it (bench.py's pushed_tail leg, so a
+      // stalled variant costs seconds, not the comparison)
+      if (const char* e = std::getenv("NKHIP_ARN_TAIL_TIMEOUT_S")) {
+        const double sec = std::atof(e);
+        if (sec > 0) {
+          const uint64_t t = uint64_t(double(ticks) * sec / device_wait_seconds());
+          tl.wait_ticks = std::min(tl.wait_ticks, t);
+          if (have_pa) tl.pa.wait_ticks = std::min(tl.pa.wait_ticks, t);
+        }
+      }
     }
     bool tail_used = false;
     int rc = P_.fused_step(Vp, cc, t + 1, V_[t + 1], 1.0, X_, G0_, nullptr, 1.0, 1.0, vout,

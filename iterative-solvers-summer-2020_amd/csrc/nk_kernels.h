@@ -27,6 +27,7 @@ bool slab_x_enabled(const nk_comm* c);
 // wall_clock64() ticks of one bounded device-side wait: NKHIP_PEER_TIMEOUT_S seconds (default
 // 20) at the device's wall-clock rate (hipDeviceAttributeWallClockRate)
 uint64_t device_wait_ticks();
+double device_wait_seconds();  // the seconds device_wait_ticks() stands for
 
 // ---------------------------------------------------------------------------------------------
 struct Field {
@@ -72,6 +73,13 @@ struct StencilArgs {
   // FDJVP/AJVP: if set, the step / scale come from the device value |z_raw|^2 (see jvp_scale)
   const double* znorm2 = nullptr;
   double omega = 0.0;
+  // FDJVP, speculative (NewtonKrylov::line_search): the first JVP of the NEXT LGMRES call, issued
+  // behind the s = 1 trial before the host has its reduction spec[0..2] = (sum F^2, max|F|,
+  // max|x|).  The pass runs only if that trial passes the Armijo test (sum F^2 <= spec_thr) and
+  // the iteration goes on (max|F| > spec_ftol); its step is the host's: omega = spec_rdiff
+  // max(1, max|x|) / max(1, max|F|), sc = omega / spec_zn, alpha = sc spec_zs.
+  const double* spec = nullptr;
+  double spec_thr = 0.0, spec_ftol = 0.0, spec_rdiff = 0.0, spec_zn = 1.0, spec_zs = 1.0;
   double theta = 0.0;  // LINOP
   // edge array of out0 (nk::edge_elems layout, below): written in-kernel for the pool vectors the
   // fused Arnoldi kernel reads block halos from (TRIAL's F, the JVP's w), so no edge_gather pass
@@ -288,6 +296,9 @@ hipError_t arnoldi_edge_launch(const ArnoldiArgs& A, double* y4, hipStream_t s);
 hipError_t arnoldi_edge_halo_launch(const ArnoldiArgs& A, const PeerArgs& pa, double* yh,
                                     hipStream_t s);
 int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset);
+// the mailbox statistics build (NKHIP_ARN_MBSTAT): halo pairs needed, not there at the first look,
+// extra polls, recomputed; -1 in other builds
+int arnoldi_mailbox_counters(int64_t out[4], bool reset);
 // Pushed halo rows (peer.hip): v's rows 0, 1 -> rows 2, 3 of prev_slot and rows ny-2, ny-1 ->
 // rows 0, 1 of next_slot (the ring neighbours' halo slots of v's pool vector, row stride ld,
 // peer memory), then a system-scope fence; nothing waits (the next all-reduce orders it).

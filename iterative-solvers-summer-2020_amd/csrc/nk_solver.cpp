@@ -547,8 +547,38 @@ int NewtonKrylov::line_search(double* s_out, double* fnorm_new, double* fmax, do
   if (o_.line_search) {
     const double phi0 = tmp_phi, derphi0 = -tmp_phi, c1 = 1e-4, amin = 1e-2;
     double alpha0 = 1.0;
+    // The next LGMRES call's first JVP (J applied to its first augmentation vector at the trial
+    // point, _gcrotmk.py:107-110 with prepend_outer_v) is queued behind this s = 1 trial, before
+    // the host reads the trial's reduction: the pass runs on the device only if the full step
+    // passes this Armijo test and the iteration goes on (the usual outcome), with the FD step
+    // the host would compute from the same values (StencilArgs::spec).  The GPU then does not
+    // idle through the host's round trip before that JVP.
+    const double thr = phi0 + c1 * alpha0 * derphi0;
+    const int K = int(outer_.size());
+    spec_.valid = false;
+    Problem::SpecJvp sp{};
+    const bool arm = P_.can_spec_jvp() && ocount_ > 0 && K > 0 && V_.size() > 1;
+    if (arm) {
+      const int slot = ohead_ % K;
+      sp = Problem::SpecJvp{outer_[slot], osig_[slot], osig_[slot] * orn_[slot], thr, f_tol_,
+                            rdiff_, V_[1]};
+      if (sp.zn != 0.0) P_.arm_spec(&sp);
+    }
     double phi_a0 = phi(alpha0);
+    P_.arm_spec(nullptr);
     if (rc) return rc;
+    if (arm && sp.zn != 0.0) {  // what the pass decided, from the same values
+      const bool ran = std::isfinite(tmp_sum) && tmp_sum <= thr && !(tmp_fmax <= f_tol_);
+      if (ran) {
+        spec_.valid = true;
+        spec_.z = sp.z;
+        spec_.zs = sp.zs;
+        spec_.zn = sp.zn;
+        spec_.w = sp.w;
+      } else {
+        E_.void_last(K_FDJVP, 1);  // a launch that did nothing
+      }
+    }
     if (phi_a0 <= phi0 + c1 * alpha0 * derphi0) {
       s = alpha0;
     } else {
@@ -608,6 +638,8 @@ int NewtonKrylov::solve(const double* x_in, double* x_out, nk_stats* st) {
   ohead_ = 0;
   const int64_t n = E_.n;
   const double f_tol = std::isnan(o_.f_tol) ? std::pow(kEps, 1.0 / 3.0) : o_.f_tol;
+  f_tol_ = f_tol;
+  spec_.valid = false;
   const double f_rtol = std::isnan(o_.f_rtol) ? INFINITY : o_.f_rtol;
   const double x_tol = std::isnan(o_.x_tol) ? INFINITY : o_.x_tol;
   const double x_rtol = std::isnan(o_.x_rtol) ? INFINITY : o_.x_rtol;

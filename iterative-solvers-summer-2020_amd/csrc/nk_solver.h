@@ -269,6 +269,18 @@ struct Problem {
   virtual void void_fused_steps(int /*count*/) {}
   virtual int set_x0(const double* /*x0*/) { return NK_OK; }   // new Newton iterate (halo)
   virtual int set_dir(const double* /*d*/) { return NK_OK; }   // new search direction (halo)
+  // Speculative first JVP of the next LGMRES call (NewtonKrylov::line_search): w = J z at the
+  // trial point x0 = xt, G0 = G of the NEXT eval(), issued by that eval right behind its
+  // reduction and before it synchronises; the pass itself decides from the reduction whether it
+  // runs (StencilArgs::spec) and computes the host's FD step.  arm_spec(nullptr) disarms.
+  struct SpecJvp {
+    const double* z;
+    double zs, zn;           // z's scale and |zs z| (the host's input(0) of the next call)
+    double thr, ftol, rdiff;  // Armijo threshold of s = 1, f_tol, rdiff
+    double* w;               // the next call's V_[1]
+  };
+  virtual bool can_spec_jvp() const { return false; }
+  virtual void arm_spec(const SpecJvp* /*sp*/) {}
 };
 
 // nonlin_solve + KrylovJacobian + lgmres(maxiter=1, outer_k, prepend_outer_v) on one Problem.
@@ -291,7 +303,8 @@ class NewtonKrylov {
  private:
   int lgmres(double tol, double* dnorm, double* dmax, double** dvec);
   // Launch JVP_j (w = V[j+1] = J z_j) and the fused multi-dot of step j; no synchronisation.
-  int issue_step(int j, const double* z, double zs, double znorm, bool dev_scale);
+  int issue_step(int j, const double* z, double zs, double znorm, bool dev_scale,
+                 bool have_w = false);
   // Device-side Arnoldi control (arnctl.hip): from step S.j (whose fused launch and reduction
   // are queued), queue fused step + reduction + control per step, one step ahead of the
   // control's status words, until the control hands a step back; then restore the host's view
@@ -322,6 +335,14 @@ class NewtonKrylov {
   std::vector<double> steps_;  // step_log()
   double fx_norm_ = 0.0;
   double rdiff_ = 0.0;
+  double f_tol_ = 0.0;
+  // the speculative first JVP of the next LGMRES call (line_search): ran on the device
+  struct {
+    bool valid = false;
+    const double* z = nullptr;
+    double zs = 0.0, zn = 0.0;
+    double* w = nullptr;
+  } spec_;
 };
 
 // Default options (SciPy newton_krylov defaults).

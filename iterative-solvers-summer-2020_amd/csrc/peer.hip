@@ -131,15 +131,18 @@ uint64_t process_nonce() {
 uint64_t wait_ticks() { return device_wait_ticks(); }
 }  // namespace
 
+double device_wait_seconds() {
+  const char* e = std::getenv("NKHIP_PEER_TIMEOUT_S");
+  const double s = (e && *e) ? std::atof(e) : 20.0;
+  return (s > 0) ? s : 20.0;
+}
+
 uint64_t device_wait_ticks() {
   int dev = 0, khz = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
     khz = 100000;  // the 100 MHz constant clock of CDNA3/4
-  const char* e = std::getenv("NKHIP_PEER_TIMEOUT_S");
-  double s = (e && *e) ? std::atof(e) : 20.0;
-  if (!(s > 0)) s = 20.0;
-  return uint64_t(s * 1e3 * double(khz));
+  return uint64_t(device_wait_seconds() * 1e3 * double(khz));
 }
 
 namespace {

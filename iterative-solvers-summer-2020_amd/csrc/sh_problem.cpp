@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "peer_dev.h"
 
@@ -283,7 +284,43 @@ int SHProblem::eval(const double* x, const double* p, double alpha, double* xt, 
   // (F may become V_0 and xt the next iterate x0: their edge rows went into the neighbours'
   // slots in the pass, before the all-reduce of the reduction below)
   if (rc) return rc;
-  return E_.reduce(nblk, 1, 3, red);
+  const SpecJvp sp = spec_;
+  spec_ = SpecJvp{};
+  if (!sp.z || !xt || dist()) return E_.reduce(nblk, 1, 3, red);
+  // the next LGMRES call's first JVP at x0 = xt, right behind the reduction it depends on (the
+  // pass decides from it whether it runs): the GPU goes on while the host reads the result
+  rc = E_.reduce_async(nblk, 1, 3, Engine::kSlotSync);
+  if (!rc) {
+    StencilArgs J;
+    J.ny = ny_;
+    J.nx = nx_;
+    J.c = c_;
+    J.out0 = sp.w;
+    set_edges(&J, sp.w);
+    J.a = field(xt, hx_);
+    J.b = field(sp.z, hz_);
+    J.p0 = G;
+    J.spec = E_.dres(Engine::kSlotSync);
+    J.spec_thr = sp.thr;
+    J.spec_ftol = sp.ftol;
+    J.spec_rdiff = sp.rdiff;
+    J.spec_zn = sp.zn;
+    J.spec_zs = sp.zs;
+    side_edges(&J, xt, sp.z);
+    rc = halo_stencil(K_FDJVP, SMode::FDJVP, J, nullptr, hz_);
+  }
+  // the reduction writes its pinned host slot itself: read it there without draining the
+  // stream, so the JVP keeps the GPU busy while the host decides and queues the next launches
+  if (!rc) rc = E_.wait_results(Engine::kSlotSync, 3);
+  if (rc) return rc;
+  std::memcpy(red, E_.hres(Engine::kSlotSync), sizeof(double) * 3);
+  return NK_OK;
+}
+
+// one slab, FD JVP, and not switched off (NKHIP_SPEC_JVP=0, read per call)
+bool SHProblem::can_spec_jvp() const {
+  const char* e = std::getenv("NKHIP_SPEC_JVP");
+  return !dist() && jvp_mode_ == NK_JVP_FD && !(e && e[0] == '0');
 }
 
 int SHProblem::jvp(const double* x0, const double* G0, const double* z, double zs, double sc,

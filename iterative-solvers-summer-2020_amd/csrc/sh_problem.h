@@ -22,6 +22,8 @@ class SHProblem final : public Problem {
   int jvp(const double* x0, const double* G0, const double* z, double zs, double sc,
           double* w) override;
   bool has_dev_scale() const override { return true; }
+  bool can_spec_jvp() const override;
+  void arm_spec(const SpecJvp* sp) override { spec_ = sp ? *sp : SpecJvp{}; }
   int jvp_dev(const double* x0, const double* G0, const double* z, const double* znorm2,
               double omega, double* w) override;
   bool has_fused(int nv) const override;
@@ -59,6 +61,7 @@ class SHProblem final : public Problem {
   int jvp_mode_;
   int status_ = NK_OK;
   double* B_ = nullptr;
+  SpecJvp spec_{};        // armed speculative JVP (z == nullptr: none), issued by the next eval
   double* hx_ = nullptr;  // halos (4 rows each: lo = rows -2,-1 ; hi = rows ny, ny+1)
   double* hz_ = nullptr;
   double* hd_ = nullptr;

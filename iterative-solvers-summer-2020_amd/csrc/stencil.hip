@@ -124,9 +124,10 @@ constexpr int kRad = (M == SMode::LAP5) ? 1 : 2;
 // norm |z_raw|^2 left by the previous fused update (KrylovJacobian.matvec with v = z_raw/|z_raw|:
 // sc = omega/|v|, step = sc/|z_raw|), so the host need not synchronise before the JVP.
 template <SMode M>
-__device__ __forceinline__ void jvp_scale(const StencilArgs& A, double* alpha, double* sc) {
+__device__ __forceinline__ bool jvp_scale(const StencilArgs& A, double* alpha, double* sc) {
   *alpha = A.alpha;
   *sc = A.sc;
+  bool go = true;  // false: a speculative JVP the trial's outcome cancelled (the pass does nothing)
   if constexpr (M == SMode::FDJVP || M == SMode::AJVP) {
     if (A.znorm2) {
       const double hn = sqrt(*A.znorm2);
@@ -140,7 +141,17 @@ __device__ __forceinline__ void jvp_scale(const StencilArgs& A, double* alpha, d
       }
     }
   }
-  if constexpr (M == SMode::FDJVP) *sc = 1.0 / *sc;  // finish() scales by the reciprocal
+  if constexpr (M == SMode::FDJVP) {
+    if (A.spec) {  // the same expressions, in the same order, as the host's (NewtonKrylov)
+      const double red0 = A.spec[0], fm = A.spec[1], xm = A.spec[2];
+      go = isfinite(red0) && red0 <= A.spec_thr && !(fm <= A.spec_ftol);
+      const double omega = A.spec_rdiff * fmax(1.0, xm) / fmax(1.0, fm);
+      *sc = omega / A.spec_zn;
+      *alpha = *sc * A.spec_zs;
+    }
+    *sc = 1.0 / *sc;  // finish() scales by the reciprocal
+  }
+  return go;
 }
 
 // The point-wise input (G0, B, u or D) is streamed once per pass: optionally non-temporal, so it
@@ -190,7 +201,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
   const int64_t cm = (cc >= 2) ? cc - 2 : cc - 2 + nx;
   const int64_t cp = (cc + 2 < nx) ? cc + 2 : cc + 2 - nx;
   double alpha, sc;
-  jvp_scale<M>(A, &alpha, &sc);
+  if (!jvp_scale<M>(A, &alpha, &sc)) return;  // uniform: a cancelled speculative JVP
 
   // the block's side columns (two each side) of an own row from the fields' edge arrays: the
   // first thread's c-2, c-1 are boundary B0's slots 0, 1, the last thread's c+2, c+3 boundary
@@ -363,7 +374,7 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
   const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
   const bool active = idx < nx * ny;
   double alpha, sc;
-  jvp_scale<M>(A, &alpha, &sc);
+  if (!jvp_scale<M>(A, &alpha, &sc)) return;  // uniform: a cancelled speculative JVP
   double red[3] = {0.0, 0.0, 0.0};
   if (active) {
     const int64_t i = idx / nx, j = idx % nx;
@@ -417,6 +428,69 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// tile kernel: the pure operators (Lap v, L v) on small grids (config 2: 1024^2 in 6.4 us by the
+// march, 4 rows per band).  A thread owns two adjacent columns of ROWS rows and issues all of its
+// loads at once (3 x 16 B per window row, as the march's ld(): columns c-2.., c.., c+2..), so a
+// launch is one round of memory latency; non-temporal stores by default.  Blocks map to rows XCD by XCD and never reversed: each
+// XCD reads the same rows every launch, whose 2 x 1 MB slice (input and output) stays in its 4 MB
+// L2 between back-to-back launches.  Same neighbour sums in the same order as the march kernel:
+// bitwise its results.
+// ------------------------------------------------------------------------------------------
+template <SMode M, int ROWS, bool NTS>
+__global__ void __launch_bounds__(256) tile_kernel(StencilArgs A, int gxt) {
+  constexpr int R = kRad<M>;
+  constexpr int NR = 2 * R + ROWS;  // window rows of ROWS output rows
+  const int64_t nx = A.nx, ny = A.ny;
+  const int64_t lb = (int64_t(blockIdx.x) % 8) * (int64_t(gridDim.x) / 8) + blockIdx.x / 8;
+  const int64_t nrb = (ny + ROWS - 1) / ROWS;
+  if (lb >= int64_t(gxt) * nrb) return;  // padding of the grid to a multiple of 8
+  const int64_t r0 = (lb / gxt) * ROWS;
+  const int64_t c0 = 2 * ((lb % gxt) * 256 + threadIdx.x);
+  if (c0 >= nx) return;
+  const int64_t cm = (c0 >= 2) ? c0 - 2 : c0 - 2 + nx;
+  const int64_t cp = (c0 + 2 < nx) ? c0 + 2 : c0 + 2 - nx;
+  double w[NR][6];
+#pragma unroll
+  for (int m = 0; m < NR; ++m) {
+    int64_t rr = r0 + m - R;
+    rr = (rr > ny + 1) ? ny + 1 : rr;  // rows past a short last block: a valid (halo) row
+    const double* p = rowp_fast(A.a, rr, ny, nx);
+    const double2 x0 = *reinterpret_cast<const double2*>(p + cm);
+    const double2 x1 = *reinterpret_cast<const double2*>(p + c0);
+    const double2 x2 = *reinterpret_cast<const double2*>(p + cp);
+    w[m][0] = x0.x; w[m][1] = x0.y; w[m][2] = x1.x; w[m][3] = x1.y; w[m][4] = x2.x; w[m][5] = x2.y;
+  }
+#pragma unroll
+  for (int t = 0; t < ROWS; ++t) {
+    Res res[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      Nb na, nb{0.0, 0.0, 0.0, 0.0};
+      if constexpr (R == 2) {
+        na.c = w[t + 2][2 + q];
+        na.a1 = (w[t + 2][1 + q] + w[t + 2][3 + q]) + (w[t + 1][2 + q] + w[t + 3][2 + q]);
+        na.dg = (w[t + 1][1 + q] + w[t + 1][3 + q]) + (w[t + 3][1 + q] + w[t + 3][3 + q]);
+        na.a2 = (w[t + 2][q] + w[t + 2][4 + q]) + (w[t][2 + q] + w[t + 4][2 + q]);
+      } else {
+        na.c = w[t + 1][2 + q];
+        na.a1 = (w[t + 1][1 + q] + w[t + 1][3 + q]) + (w[t][2 + q] + w[t + 2][2 + q]);
+        na.dg = 0.0;
+        na.a2 = 0.0;
+      }
+      res[q] = finish<M>(A, na, nb, 0.0, 0.0, 1.0);
+    }
+    if (r0 + t < ny) {
+      dv2* o = reinterpret_cast<dv2*>(A.out0 + (r0 + t) * nx + c0);
+      const dv2 v{res[0].o0, res[1].o0};
+      if constexpr (NTS)
+        __builtin_nontemporal_store(v, o);
+      else
+        *o = v;
+    }
+  }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int env_int(const char* name, int dflt) {
@@ -439,6 +513,31 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
       if (f->base && !f->lo) {
         f->lo = f->base + (A.ny - 2) * A.nx;
         f->hi = f->base;
+      }
+    }
+    // The pure operators on a grid of at most NKHIP_TILE_MAX points (default 2^21: 16.8 MB for
+    // input and output at 1024^2, L2-resident per XCD): one row per thread, the tile kernel
+    if constexpr (M == SMode::LAP5 || M == SMode::SH13) {
+      static const int64_t tile_max = env_int("NKHIP_TILE_MAX", 1 << 21);
+      if (A.nx * A.ny <= tile_max && !A.E0 && !A.PS0[0]) {
+        // rows per thread and the store policy (NKHIP_TILE_ROWS 1 / 2 / 4, NKHIP_TILE_NT): at
+        // 1024^2, rocprofv3, one box (profiles/r05_config2.md): march 6.43 us; rows 1 / 2 / 4
+        // 5.93 / 5.13 / 5.21 us with plain stores, 5.18-5.41 / 4.83 / 4.80-4.86 us non-temporal
+        static const int rows = env_int("NKHIP_TILE_ROWS", 2);
+        static const bool nts = env_int("NKHIP_TILE_NT", 1) != 0;
+        const int rt = (rows == 4 || rows == 2) ? rows : 1;
+        const int gxt = int((A.nx / 2 + 255) / 256);
+        const int64_t nb = int64_t(gxt) * ((A.ny + rt - 1) / rt);
+        if (nblk) *nblk = nb;
+        const dim3 grid{unsigned((nb + 7) / 8 * 8), 1u, 1u};
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, gxt); };
+        if (rt == 4)
+          nts ? go(tile_kernel<M, 4, true>) : go(tile_kernel<M, 4, false>);
+        else if (rt == 2)
+          nts ? go(tile_kernel<M, 2, true>) : go(tile_kernel<M, 2, false>);
+        else
+          nts ? go(tile_kernel<M, 1, true>) : go(tile_kernel<M, 1, false>);
+        return hipGetLastError();
       }
     }
     // Row band per block: a multiple of the ring length RING (the unroll of the walk), aiming at

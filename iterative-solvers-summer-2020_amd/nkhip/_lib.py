@@ -100,6 +100,7 @@ SIGNATURES = [
     ("nk_maxpy", C.c_int, [C.POINTER(_P), C.POINTER(_D), _I32, _P, _I64, _P]),
     ("nk_stream_copy", C.c_int, [_P, _P, _I64, _P]),
     ("nk_debug_bounds", C.c_int, [C.POINTER(_I64), C.POINTER(_I32), _I32]),
+    ("nk_debug_mailbox", C.c_int, [C.POINTER(_I64), _I32]),
     ("nk_comm_unique_id_bytes", C.c_int, []),
     ("nk_comm_get_unique_id", C.c_int, [_P]),
     ("nk_comm_create_rccl", C.c_int, [C.POINTER(_P), _P, _I32, _I32]),

@@ -74,6 +74,12 @@ def main():
             for i in range(3):
                 one(i)
             torch.cuda.synchronize()
+            mbstat = os.environ.get("ARN_MBSTAT") == "1"  # the mailbox statistics build
+            if mbstat:
+                import ctypes as C
+                from nkhip import _lib
+                cnt = (C.c_int64 * 4)()
+                _lib.lib.nk_debug_mailbox(cnt, 1)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 20
             a.record()
@@ -85,6 +91,11 @@ def main():
             byt = 8.0 * n * (nv + 4 + (1 if ext else 0))
             out.append({"nv": nv, "ext": ext, "us": round(us, 2),
                         "GBps": round(byt / us / 1e3, 1), "frac": round(byt / us / 1e3 / 8000, 3)})
+            if mbstat:
+                rc = _lib.lib.nk_debug_mailbox(cnt, 1)
+                out[-1]["mailbox_per_launch"] = (
+                    {k: cnt[i] / reps for i, k in enumerate(("needed", "late", "extra_polls",
+                                                             "recomputed"))} if rc == 0 else rc)
             print(json.dumps(out[-1]), flush=True)
     tag = os.environ.get("ARN_TAG", "")
     if tag:

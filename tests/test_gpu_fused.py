@@ -130,7 +130,7 @@ def test_fused_slabs_match_single_slab(nranks, ny_total, nx, overlap, devctl, mo
     devctl "1" (the default with a communicator): the Arnoldi control runs on the device, every
     rank's control kernel taking the same decisions from the same all-reduced results."""
     import nkhip
-    from conftest import run_slabs
+    from conftest import load_golden, run_slabs
     # "1": interior rows on a side stream during the edge exchange, edge bands after it
     monkeypatch.setenv("NKHIP_SLAB_OVERLAP", overlap)
     monkeypatch.setenv("NKHIP_DEVCTL", devctl)
@@ -205,6 +205,45 @@ def test_edges_identical_solve(ny, nx, monkeypatch):
     _, b, sb, pb = _step(ny, nx, fused=True)
     assert np.array_equal(a, b) and sa == sb
     assert pb["arnoldi_fused"]["launches"] > 0
+
+
+@pytest.mark.parametrize("ny,nx,fused", [(64, 64, True), (61, 61, False), (256, 256, True),
+                                         (128, 600, True), (96, 130, False)])
+def test_speculative_jvp_identical(ny, nx, fused, monkeypatch):
+    """The line search's speculative first JVP of the next LGMRES call (NewtonKrylov::line_search:
+    queued behind the s = 1 trial, run by the device only if that trial passes the Armijo test and
+    the iteration goes on, with the host's FD step from the same reduction values) leaves the
+    solve bitwise as without it (NKHIP_SPEC_JVP=0): same roots, same Newton / F-eval / JVP
+    counts, and the same FD-JVP launch count (a pass the trial cancelled leaves the profile)."""
+    monkeypatch.setenv("NKHIP_SPEC_JVP", "0")
+    _, a, sa, pa = _step(ny, nx, fused=fused, steps=2)
+    monkeypatch.delenv("NKHIP_SPEC_JVP")
+    _, b, sb, pb = _step(ny, nx, fused=fused, steps=2)
+    assert np.array_equal(a, b) and sa == sb
+    assert sum(s["nit"] for s in sb) > 2  # line searches that armed it
+    assert pa["sh_fdjvp"]["launches"] == pb["sh_fdjvp"]["launches"]
+
+
+def test_speculative_jvp_backtracking(monkeypatch):
+    """The same on the reference's backtracking step (nk_n61_amp3_backtrack: 5 of 13 Newton
+    iterations backtrack, so the speculative pass is cancelled there and runs elsewhere)."""
+    import nkhip
+    from conftest import load_golden
+    z = load_golden("nk_n61_amp3_backtrack")
+    N = int(z["N"])
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NKHIP_SPEC_JVP", mode)
+        m = nkhip.SwiftHohenberg(N=N, d=float(z["d"]), k=float(z["k"]), r=float(z["r"]),
+                                 g=float(z["g"]), f_tol=None if np.isnan(z["f_tol"])
+                                 else float(z["f_tol"]))
+        U = m.step(torch.as_tensor(z["traj"][0].reshape(N, N), device="cuda"))
+        out[mode] = (U.cpu().numpy(), dict(m.last_stats), list(m.step_log()),
+                     m.kernel_profile()["sh_fdjvp"]["launches"])
+        m.close()
+    assert np.array_equal(out["0"][0], out["1"][0])
+    assert out["0"][1:] == out["1"][1:]
+    assert sum(s < 1 for s in out["1"][2]) >= 1
 
 
 @pytest.mark.parametrize("ny,nx", [(64, 64), (128, 60), (96, 130), (256, 256), (40, 512),

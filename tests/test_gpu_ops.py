@@ -179,3 +179,22 @@ def test_config2_1024(op):
         y = nkhip.sh13_apply(v, h, r).cpu().numpy().reshape(-1)
         ref = sh_oracle.sh13(v_np, n, n, h, r)
     assert np.abs(y - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("op", ["lap5", "sh13"])
+@pytest.mark.parametrize("ny,nx", [(2048, 1024), (2056, 1024), (6, 8), (3, 10)])
+def test_tile_and_march_operators(op, ny, nx):
+    """The pure operators take the one-row-per-thread tile kernel up to 2^21 points (config 2's
+    1024^2) and the march kernel above: both against the oracle stencils on either side of the
+    switch (2048 x 1024 = 2^21: tile; 2056 x 1024: march) and on the smallest grids."""
+    import nkhip
+    h, r = 0.625, 0.01
+    v_np = np.random.default_rng(ny + nx).standard_normal(ny * nx)
+    v = torch.as_tensor(v_np.reshape(ny, nx), device="cuda")
+    if op == "lap5":
+        y = nkhip.lap5_apply(v, 1 / h ** 2).cpu().numpy().reshape(-1)
+        ref = sh_oracle.lap5(v_np, ny, nx, 1 / h ** 2)
+    else:
+        y = nkhip.sh13_apply(v, h, r).cpu().numpy().reshape(-1)
+        ref = sh_oracle.sh13(v_np, ny, nx, h, r)
+    assert np.abs(y - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
