@@ -452,17 +452,24 @@ __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int
 // must keep (an SGPR, or a VGPR lane when it spills) instead of re-reading it from the kernel
 // arguments
 typedef int ix_t;
+// ARN_OPQ 2 also pins the stencil coefficients and the x0 pointer (doubles / pointers through an
+// "s" asm constraint): the bounds-checked build of that produced NaN at nv 25-30 on the mailbox
+// instantiation without a single out-of-range index (round 5: ARN_OPQ 1 and 0 are clean), so the
+// default pins the 32-bit grid scalars only
+#ifndef ARN_OPQ  // 2: grid scalars, stencil coefficients and x0 pinned; 1: grid scalars; 0: none
+#define ARN_OPQ 1
+#endif
 __device__ __forceinline__ int opaque_s(int x) {
   x = __builtin_amdgcn_readfirstlane(x);
-  asm volatile("" : "+s"(x));
+  if constexpr (ARN_OPQ >= 1) asm volatile("" : "+s"(x));
   return x;
 }
 __device__ __forceinline__ double opaque_d(double x) {
-  asm volatile("" : "+s"(x));
+  if constexpr (ARN_OPQ >= 2) asm volatile("" : "+s"(x));
   return x;
 }
 __device__ __forceinline__ const double* opaque_p(const double* p) {
-  asm volatile("" : "+s"(p));
+  if constexpr (ARN_OPQ >= 2) asm volatile("" : "+s"(p));
   return p;
 }
 

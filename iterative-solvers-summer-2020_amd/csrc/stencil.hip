@@ -432,10 +432,10 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
 // tile kernel: the pure operators (Lap v, L v) on small grids (config 2: 1024^2 in 6.4 us by the
 // march, 4 rows per band).  A thread owns two adjacent columns of ROWS rows and issues all of its
 // loads at once (3 x 16 B per window row, as the march's ld(): columns c-2.., c.., c+2..), so a
-// launch is one round of memory latency; non-temporal stores by default.  Blocks map to rows XCD by XCD and never reversed: each
-// XCD reads the same rows every launch, whose 2 x 1 MB slice (input and output) stays in its 4 MB
-// L2 between back-to-back launches.  Same neighbour sums in the same order as the march kernel:
-// bitwise its results.
+// launch is one round of memory latency; non-temporal stores by default.  Blocks map to rows
+// XCD by XCD and never reversed: each XCD reads the same rows every launch, whose 2 x 1 MB slice
+// (input and output) stays in its 4 MB L2 between back-to-back launches.  Same neighbour sums in
+// the same order as the march kernel: bitwise its results.
 // ------------------------------------------------------------------------------------------
 template <SMode M, int ROWS, bool NTS>
 __global__ void __launch_bounds__(256) tile_kernel(StencilArgs A, int gxt) {
