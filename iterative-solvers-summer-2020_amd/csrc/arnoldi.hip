@@ -231,7 +231,8 @@ __device__ unsigned long long g_mb_stat[4];
 #else
 #define MB_STAT(i, v) ((void)0)
 #endif
-__device__ __forceinline__ uint32_t mb_off(uint32_t blk, uint32_t T, uint32_t t, int side, int comp) {
+__device__ __forceinline__ uint32_t mb_off(uint32_t blk, uint32_t T, uint32_t t, int side,
+                                           int comp) {
   return (((blk * T + t) * 4) + uint32_t(side * 2 + comp)) * 16u;  // < mb_cap * 8 < 2^32
 }
 __device__ __forceinline__ bool mb_tag_ok(const u32x4& a, uint64_t tag) {
@@ -459,11 +460,16 @@ typedef int ix_t;
 #ifndef ARN_OPQ  // 2: grid scalars, stencil coefficients and x0 pinned; 1: grid scalars; 0: none
 #define ARN_OPQ 1
 #endif
+template <bool PIN = true>
 __device__ __forceinline__ int opaque_s(int x) {
   x = __builtin_amdgcn_readfirstlane(x);
-  if constexpr (ARN_OPQ >= 1) asm volatile("" : "+s"(x));
+  if constexpr (PIN && ARN_OPQ >= 1) asm volatile("" : "+s"(x));
   return x;
 }
+// the basis lengths whose kernels pin them: not nv >= 34, at the register limit (n35 spills
+// either way, and 6 % slower with the scalars pinned; round 5, profiles/r05_arnoldi_short_end.md)
+template <int NV>
+constexpr bool kPinScalars = NV <= 33;
 __device__ __forceinline__ double opaque_d(double x) {
   if constexpr (ARN_OPQ >= 2) asm volatile("" : "+s"(x));
   return x;
@@ -703,7 +709,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   // scalars opaque: the compiler keeps them in registers instead of reloading them from the
   // kernel arguments inside the row loop (every such reload is a scalar load whose lgkmcnt wait
   // also drains the wave's LDS queue; ~20 per row at nv 19-24 before)
-  const ix_t nx = opaque_s(ix_t(A.nx)), ny = opaque_s(ix_t(A.ny));
+  const ix_t nx = opaque_s<kPinScalars<NV>>(ix_t(A.nx));
+  const ix_t ny = opaque_s<kPinScalars<NV>>(ix_t(A.ny));
   const ix_t B0 = grp * WB * kSW;        // the block's first column
   const ix_t c = B0 + wid * kSW + 2 * l;  // columns past nx compute wrapped columns, masked
   const ix_t col = c % nx;                // nx even: c and c+1 wrap together
@@ -713,8 +720,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const ix_t hc = (hh < 2) ? B0 - 2 + hh : B0 + WB * kSW - 2 + hh;
   const ix_t hcol = ((hc % nx) + nx) % nx;
   const ix_t rend = (A.r_end >= 0) ? ix_t(A.r_end) : ny;
-  const ix_t r0 = opaque_s(ix_t(A.r_begin) + band * A.RY);
-  const ix_t r1 = opaque_s((r0 + A.RY < rend) ? r0 + A.RY : rend);
+  const ix_t r0 = opaque_s<kPinScalars<NV>>(ix_t(A.r_begin) + band * A.RY);
+  const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
   const ix_t nrows = r1 - r0;
   // the stencil coefficients in registers for the whole loop (re-read from the kernel
   // arguments per row otherwise: a scalar load and an lgkmcnt wait each)
@@ -783,7 +790,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const ix_t nelem = ny * nx, eelem = edge_elems(ny, nx);
   const bool eL = own && (c % kEdgeW == 0);
   const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
-  const ix_t ebo = eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
+  const ix_t ebo =
+      eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
   const bool eOn = eL || eR;
   const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
   const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
@@ -1029,7 +1037,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const bool st = own && hf == 0 && q >= r0 && q < r1;
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
-                                           CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
+                                           CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0,
+                                           kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)  // wave-uniform
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
@@ -1068,7 +1077,9 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           CO((in && hf == 0) ? uint32_t(r * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
+                                           CO((in && hf == 0) ? uint32_t(r * nx + col) * 8u : kOOB,
+                                              nelem),
+                                           0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in && hf == 0, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
@@ -1225,25 +1236,27 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   __shared__ double hpart[2][W][4];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = blockIdx.x;
-  const int64_t bpx = gridDim.x / 8;  // XCD-aware: each XCD gets a contiguous run of blocks
-  const int64_t L = (b % 8) * bpx + b / 8;
-  const int64_t ngroups = (A.strips + W - 1) / W;
+  const ix_t b = blockIdx.x;
+  const ix_t bpx = gridDim.x / 8;  // XCD-aware: each XCD gets a contiguous run of blocks
+  const ix_t L = (b % 8) * bpx + b / 8;
+  const ix_t ngroups = (A.strips + W - 1) / W;
   if (L >= ngroups * A.nbands) return;
-  const int64_t band = L / ngroups, grp = L % ngroups;
-  const int64_t gw = L * W + wid;
-  const int64_t nx = A.nx, ny = A.ny;
-  const int64_t B0 = grp * W * kWW;
-  const int64_t c = B0 + wid * kWW + 2 * lane;
-  const int64_t col = c % nx;
+  const ix_t band = L / ngroups, grp = L % ngroups;
+  const ix_t gw = L * W + wid;
+  // 32-bit row / column arithmetic with the grid scalars pinned, as in arnoldi_kernel
+  const ix_t nx = opaque_s<kPinScalars<NV>>(ix_t(A.nx));
+  const ix_t ny = opaque_s<kPinScalars<NV>>(ix_t(A.ny));
+  const ix_t B0 = grp * W * kWW;
+  const ix_t c = B0 + wid * kWW + 2 * lane;
+  const ix_t col = c % nx;
   const bool own = c < nx;
   const int hh = lane & 3;  // block halo: columns B0-2, B0-1, B0 + 128 W, +1
-  const int64_t hc = (hh < 2) ? B0 - 2 + hh : B0 + W * kWW - 2 + hh;
-  const int64_t hcol = ((hc % nx) + nx) % nx;
-  const int64_t rend = (A.r_end >= 0) ? A.r_end : ny;
-  const int64_t r0 = A.r_begin + band * A.RY;
-  const int64_t r1 = (r0 + A.RY < rend) ? r0 + A.RY : rend;
-  const int64_t nrows = r1 - r0;
+  const ix_t hc = (hh < 2) ? B0 - 2 + hh : B0 + W * kWW - 2 + hh;
+  const ix_t hcol = ((hc % nx) + nx) % nx;
+  const ix_t rend = (A.r_end >= 0) ? ix_t(A.r_end) : ny;
+  const ix_t r0 = opaque_s<kPinScalars<NV>>(ix_t(A.r_begin) + band * A.RY);
+  const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
+  const ix_t nrows = r1 - r0;
   const SHCoef& K = A.k;
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
@@ -1276,29 +1289,29 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     hcf = cf;
   }
   const bool useE = A.E[0] != nullptr;
-  const int64_t nbE = edge_groups(nx);
-  const int64_t nelem = ny * nx, eelem = edge_elems(ny, nx);
-  const int64_t bL = B0 / kEdgeW, bR = ((B0 + W * kWW) / kEdgeW) % nbE;
+  const ix_t nbE = edge_groups(nx);
+  const ix_t nelem = ny * nx, eelem = edge_elems(ny, nx);
+  const ix_t bL = B0 / kEdgeW, bR = ((B0 + W * kWW) / kEdgeW) % nbE;
   const bool eL = own && (c % kEdgeW == 0);
   const bool eR = own && ((c + 2) % kEdgeW == 0 || c + 2 == nx);
-  const int64_t ebo =
+  const ix_t ebo =
       eL ? (c / kEdgeW) * 4 + 2 : (eR ? ((c + 2 == nx) ? 0 : (c + 2) / kEdgeW) * 4 : 0);
   const bool eOn = eL || eR;
   const __amdgpu_buffer_rsrc_t rEv = rsrc(A.Eout_v, A.Eout_v ? nbE * ny * 4 : 0);
   const __amdgpu_buffer_rsrc_t rEw = rsrc(A.Eout_w, A.Eout_w ? nbE * ny * 4 : 0);
-  auto eoff = [&](int64_t q) -> uint32_t {
+  auto eoff = [&](ix_t q) -> uint32_t {
     return eOn ? uint32_t(CI((ebo / 4) * ny * 4 + q * 4 + (ebo & 3), eelem - 1) * 8) : kOOB;
   };
   const double* hxp = (EXT && lane >= 4) ? A.z : A.x0;  // lanes 0-3: x0 halo, 4-7: z halo
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
-  const int64_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
-  auto wrap = [&](int64_t q) -> int64_t {
+  const ix_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
+  auto wrap = [&](ix_t q) -> ix_t {
     q = (q > r1 + 1) ? r1 + 1 : q;
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
-  auto halo_row = [&](int64_t q) -> bool {
-    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
+  auto halo_row = [&](ix_t q) -> bool {
+    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;
     return slab && (qc < 0 || qc >= ny);
   };
 
@@ -1306,26 +1319,26 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   // left halo pair, wave W-1's lane 63 the last pair and the right halo pair
   constexpr int BW = W * kWW;
   constexpr bool mb = MB && !EXT;
-  const int64_t mbT = A.RY + 8;
+  const ix_t mbT = A.RY + 8;
   const __amdgpu_buffer_rsrc_t rmb = rsrc(A.mb, mb ? A.mb_cap : 0);
   const uint64_t tag = A.mb_tag;
   const bool needL = mb && wid == 0 && lane == 0, needR = mb && wid == W - 1 && lane == 63;
-  const int64_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
+  const ix_t Lnb = band * ngroups + (needL ? (grp + ngroups - 1) % ngroups : (grp + 1) % ngroups);
   const int nside = needL ? 1 : 0;
   const bool prod = needL || needR;
   const int pside = needL ? 0 : 1;
-  const int64_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;
+  const ix_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;
   bool mb_dead = A.mb_recompute;
-  auto mb_need = [&](int64_t q) -> bool { return (needL || needR) && !halo_row(q); };
-  auto poll = [&](int64_t q, u32x4* a, u32x4* b) {
+  auto mb_need = [&](ix_t q) -> bool { return (needL || needR) && !halo_row(q); };
+  auto poll = [&](ix_t q, u32x4* a, u32x4* b) {
     const bool on = mb_need(q) && !mb_dead;
     const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
     ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
     *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
     *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
   };
-  auto recompute = [&](int64_t q) -> dv2 {  // push()'s update sum, entry order (rolled loop)
-    const int64_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
+  auto recompute = [&](ix_t q) -> dv2 {  // push()'s update sum, entry order (rolled loop)
+    const ix_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
     dv2 v{0.0, 0.0};
 #pragma unroll 1
     for (int e = 0; e <= NV; ++e) {
@@ -1336,7 +1349,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     return v;
   };
-  auto mb_halo = [&](int64_t q, u32x4 a, u32x4 b) -> dv2 {
+  auto mb_halo = [&](ix_t q, u32x4 a, u32x4 b) -> dv2 {
     const bool need = mb_need(q);
     bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
     dv2 h{mb_val(a), mb_val(b)};
@@ -1363,29 +1376,29 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     double hv, hx;
     bool own;
   };
-  auto load = [&](Slot& s, int64_t q) {
-    const int64_t qq = wrap(q);
-    const int64_t o = CI(qq * nx + col, nelem - 1);
-    const int64_t qc = (q > r1 + 1) ? r1 + 1 : q;
+  auto load = [&](Slot& s, ix_t q) {
+    const ix_t qq = wrap(q);
+    const ix_t o = CI(qq * nx + col, nelem - 1);
+    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;
     const bool hrow = halo_row(q);
-    const int64_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
-    const int64_t yo = CI(hq * yld + col, 4 * yld - 1);
+    const ix_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
+    const ix_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const double* a = src(e) + o;
       if (e == EX) a = hrow ? yhb + yo : a;
       s.e[e] = gld2<NT>(a);
     }
-    const int64_t ho = CI(qq * nx + hcol, nelem);
+    const ix_t ho = CI(qq * nx + hcol, nelem);
     if constexpr (!EXT && !mb) {
-      const int64_t eo = CI(useE ? ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh : 0, eelem);
+      const ix_t eo = CI(useE ? ((((hh < 2) ? bL : bR) * ny + qq) << 2) + hh : 0, eelem);
       s.hv = gld(useE ? hE + eo : hp + ho);
     }
-    const int64_t hyo = CI(hq * yld + hcol, 4 * yld);
+    const ix_t hyo = CI(hq * yld + hcol, 4 * yld);
     s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? A.x0 : hxp + ho));
     s.own = !hrow;
   };
-  auto stash = [&](const Slot& s, const dv2& g, int64_t q) {
+  auto stash = [&](const Slot& s, const dv2& g, ix_t q) {
     dv2 (*d)[64] = lg[(q - r0) & 1];
 #pragma unroll
     for (int e = 0; e < NV; ++e) d[e][lane] = s.e[e];
@@ -1396,7 +1409,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
 #pragma unroll
   for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
   dv2 gq{0.0, 0.0};
-  auto push = [&](const Slot& s, int64_t q) {
+  auto push = [&](const Slot& s, ix_t q) {
     dv2 v{0.0, 0.0};
 #pragma unroll
     for (int e = 0; e <= NV; ++e) {  // entry order (the slab edge kernel sums the same way)
@@ -1472,7 +1485,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     vw[4] = v;
     const bool st = own && q >= r0 && q < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
-                                           CO(st ? uint32_t((q * nx + col) * 8) : kOOB, nelem), 0, kOutPol);
+                                           CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0,
+                                           kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS, A.hs_ld, q, ny, col, st, v);
     if (A.Eout_v)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rEv,
@@ -1489,7 +1503,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
 #pragma unroll
   for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
   const double zs = a_alpha * isc;
-  auto centre = [&](int64_t r) {  // closed-form FD quotient as in arnoldi_kernel
+  auto centre = [&](ix_t r) {  // closed-form FD quotient as in arnoldi_kernel
     const dv2 (*d)[64] = lg[(r - r0) & 1];
     const dv2 x0r = d[NV][lane];
     dv2 wo;
@@ -1507,7 +1521,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     const bool in = own && r < r1;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
-                                           CO(in ? uint32_t((r * nx + col) * 8) : kOOB, nelem), 0, kOutPol);
+                                           CO(in ? uint32_t(r * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in, wo);
     if (A.Eout_w)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rEw,
@@ -1524,7 +1538,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     aw[NV + 1] = __builtin_fma(vm.y, vm.y, __builtin_fma(vm.x, vm.x, aw[NV + 1]));
     aw[NV + 2] = __builtin_fma(wm.y, wm.y, __builtin_fma(wm.x, wm.x, aw[NV + 2]));
   };
-  auto push_h2 = [&](const Slot& s, int64_t q) {
+  auto push_h2 = [&](const Slot& s, ix_t q) {
     const dv2 h2 = push(s, q);
     h2w[0] = h2w[1];
     h2w[1] = h2w[2];
@@ -1565,10 +1579,10 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
         fixup(hw[3], h2w[1], mb_halo(r0, a1, b1));
       }
     }
-    for (int64_t t0 = 0; t0 < nrows; t0 += RR) {  // no branch inside a group (see arnoldi_kernel)
+    for (ix_t t0 = 0; t0 < nrows; t0 += RR) {  // no branch inside a group (see arnoldi_kernel)
 #pragma unroll
       for (int k = 0; k < RR; ++k) {
-        const int64_t r = r0 + t0 + k;
+        const ix_t r = r0 + t0 + k;
         u32x4 ma, mb2;
         if constexpr (mb) poll(r + 1, &ma, &mb2);
         load(S[(k + PF) % RR], r + 2 + PF);

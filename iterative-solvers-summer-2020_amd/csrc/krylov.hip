@@ -144,7 +144,8 @@ __global__ void __launch_bounds__(BS) mdot_kernel(const double* a, const double*
 template <bool VEC, bool NT, int UNR>
 __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in, double cin,
                                                    VecList P, int np, int64_t n, int cpb,
-                                                   double* partial, bool rev, const double* prm) {
+                                                   double* partial, bool rev, const double* prm,
+                                                   EdgeOut eo) {
   // prm (device-side Arnoldi control): cin and the coefficients from the control's parameter
   // block; a step the control handed back does nothing
   if (prm) {
@@ -197,6 +198,21 @@ __global__ void __launch_bounds__(BS) combo_kernel(double* out, const double* in
       for (int k = 0; k < PAIRS; ++k) {
         acc[k].x += c * pv[k].x;
         acc[k].y += c * pv[k].y;
+      }
+    }
+    if (eo.E) {  // out's edge array (edge_gather_kernel's layout): the pairs at group borders
+      const uint32_t nx = uint32_t(eo.nx), ny = uint32_t(eo.ny);
+      uint32_t q = uint32_t(base) / nx, c = uint32_t(base) - q * nx;
+#pragma unroll
+      for (int k = 0; k < PAIRS; ++k) {
+        if (base + k * 2 * BS < n) {
+          const dv2 ev = {acc[k].x, acc[k].y};
+          if (c % kEdgeW == 0)
+            reinterpret_cast<dv2*>(eo.E)[2 * ((c / kEdgeW) * ny + q) + 1] = ev;
+          if ((c + 2) % kEdgeW == 0 || c + 2 == nx)
+            reinterpret_cast<dv2*>(eo.E)[2 * ((c + 2 == nx ? 0 : (c + 2) / kEdgeW) * ny + q)] = ev;
+        }
+        for (c += 2 * BS; c >= nx; c -= nx) ++q;
       }
     }
 #pragma unroll
@@ -343,8 +359,11 @@ hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int n
 
 namespace {
 hipError_t combo_any(double* out, const double* in, double cin, const VecList& P, int np,
-                     int64_t n, double* partial, hipStream_t s, int64_t* nblk, const double* prm) {
+                     int64_t n, double* partial, hipStream_t s, int64_t* nblk, const double* prm,
+                     const EdgeOut& eo) {
   if (np < 0 || np > kMaxVec) return hipErrorInvalidValue;
+  if (eo.E && (eo.nx < 4 || eo.nx % 2 || eo.ny < 1 || eo.nx * eo.ny != n || n >= (int64_t(1) << 31)))
+    return hipErrorInvalidValue;
   static const int target = env_int("NKHIP_COMBO_BLOCKS", 1 << 30);
   int cpb = 0;
   const int64_t nb = krylov_grid(n, &cpb, target);
@@ -358,33 +377,34 @@ hipError_t combo_any(double* out, const double* in, double cin, const VecList& P
   if (nb <= kSmallChunks) {  // small vectors: 8 basis vectors' loads in flight per batch
     if (vec)
       hipLaunchKernelGGL((combo_kernel<true, false, 8>), grid, block, 0, s, out, in, cin, P, np, n,
-                         cpb, partial, rev, prm);
+                         cpb, partial, rev, prm, eo);
     else
       hipLaunchKernelGGL((combo_kernel<false, false, 8>), grid, block, 0, s, out, in, cin, P, np,
-                         n, cpb, partial, rev, prm);
+                         n, cpb, partial, rev, prm, eo);
   } else if (vec && nt) {
     hipLaunchKernelGGL((combo_kernel<true, true, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev, prm);
+                       cpb, partial, rev, prm, eo);
   } else if (vec) {
     hipLaunchKernelGGL((combo_kernel<true, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev, prm);
+                       cpb, partial, rev, prm, eo);
   } else {
     hipLaunchKernelGGL((combo_kernel<false, false, 2>), grid, block, 0, s, out, in, cin, P, np, n,
-                       cpb, partial, rev, prm);
+                       cpb, partial, rev, prm, eo);
   }
   return hipGetLastError();
 }
 }  // namespace
 
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
-                        int64_t n, double* partial, hipStream_t s, int64_t* nblk) {
-  return combo_any(out, in, cin, P, np, n, partial, s, nblk, nullptr);
+                        int64_t n, double* partial, hipStream_t s, int64_t* nblk,
+                        const EdgeOut& eo) {
+  return combo_any(out, in, cin, P, np, n, partial, s, nblk, nullptr, eo);
 }
 
 hipError_t combo_prm_launch(double* out, const double* in, const double* prm, const VecList& P,
                             int np, int64_t n, hipStream_t s) {
   if (!prm || np > kArnMaxNV) return hipErrorInvalidValue;
-  return combo_any(out, in, 0.0, P, np, n, nullptr, s, nullptr, prm);
+  return combo_any(out, in, 0.0, P, np, n, nullptr, s, nullptr, prm, EdgeOut{});
 }
 
 hipError_t reduce_final_launch(const double* partial, int64_t nblk, int nsum, int nv,

@@ -282,10 +282,11 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     }
     if (lag_step) {
       // -- v_{j+1} = tau w - V h (no reduction), then step j+1 right away
+      const EdgeOut eo = P_.edge_out(w);  // v_{j+1}, a basis vector of later fused steps
       rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
-        return combo_launch(w, w, tau, U, j + 1, n, nullptr, E_.s, &nblk);
+        return combo_launch(w, w, tau, U, j + 1, n, nullptr, E_.s, &nblk, eo);
       });
-      if (!rc) rc = P_.publish_edges(w);  // v_{j+1}, a basis vector of later fused steps
+      if (!rc) rc = P_.publish_edges(w, eo.E != nullptr);
       if (rc) return rc;
       const double* z;
       double zs, zn;
@@ -319,11 +320,13 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
       continue;
     }
     // -- v_{j+1} = tau w - V h and its exact |v_{j+1}|^2 before the next JVP
+    // v_{j+1}'s edge array (written by the combination) and pushed edge rows, before the
+    // all-reduce below orders them
+    const EdgeOut eo = P_.edge_out(w);
     rc = E_.launch(K_COMBO, 8.0 * n * (j + 3), [&] {
-      return combo_launch(w, w, tau, U, j + 1, n, E_.partial(), E_.s, &nblk);
+      return combo_launch(w, w, tau, U, j + 1, n, E_.partial(), E_.s, &nblk, eo);
     });
-    // v_{j+1}'s edge array (and pushed edge rows), before the all-reduce below orders them
-    if (!rc) rc = P_.publish_edges(w);
+    if (!rc) rc = P_.publish_edges(w, eo.E != nullptr);
     // only |v_{j+1}|^2 is used (a non-finite v shows up in it): one sum, one all-reduce on N GPUs
     if (!rc) rc = E_.reduce_async(nblk, 1, 1, Engine::kSlotCombo);
     if (rc) return rc;
@@ -374,12 +377,14 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
   }
   int64_t nblk = 0;
   double* d = outer_[slot];
-  rc = E_.launch(K_COMBO, 8.0 * n * (j + 2), [&] {
-    return combo_launch(d, nullptr, 0.0, Z, j + 1, n, E_.partial(), E_.s, &nblk);
-  });
   // d: the line search's direction and the newest augmentation vector (z of later fused steps):
-  // its edge array, and on pushed-halo slabs its edge rows, before the all-reduce below
-  if (!rc) rc = P_.publish_edges(d);
+  // its edge array (written by the combination), and on pushed-halo slabs its edge rows, before
+  // the all-reduce below
+  const EdgeOut eo = P_.edge_out(d);
+  rc = E_.launch(K_COMBO, 8.0 * n * (j + 2), [&] {
+    return combo_launch(d, nullptr, 0.0, Z, j + 1, n, E_.partial(), E_.s, &nblk, eo);
+  });
+  if (!rc) rc = P_.publish_edges(d, eo.E != nullptr);
   if (rc) return rc;
   double r2[2];
   rc = E_.reduce(nblk, 1, 2, r2);

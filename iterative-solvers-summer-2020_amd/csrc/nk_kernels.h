@@ -132,10 +132,18 @@ int64_t krylov_grid(int64_t n, int* cpb, int64_t target_blocks);
 // partial[(i)*nblk + b]: a.p_i for i < np, g.p_i at np+i (g may be null -> zeros), a.a at 2np.
 hipError_t mdot_launch(const double* a, const double* g, const VecList& P, int np, int64_t n,
                        double* partial, hipStream_t s, int64_t* nblk);
+// out's edge array (the fused kernel's block halos, kEdgeW below), written by the pass that
+// writes out: E (edge_elems(ny, nx) values), out's row length nx (even) and row count ny.
+struct EdgeOut {
+  double* E = nullptr;
+  int64_t nx = 0, ny = 0;
+};
 // out = cin*in + sum_i c_i p_i (in may be null); partial: [0] sum out^2, [1] max|out|.
 // out may alias `in` or any p_i (element-wise, each element read and written by one thread).
+// eo.E: also write out's edge array (n == eo.nx eo.ny < 2^31), so no edge_gather pass follows.
 hipError_t combo_launch(double* out, const double* in, double cin, const VecList& P, int np,
-                        int64_t n, double* partial, hipStream_t s, int64_t* nblk);
+                        int64_t n, double* partial, hipStream_t s, int64_t* nblk,
+                        const EdgeOut& eo = EdgeOut{});
 // The same under device-side Arnoldi control: out = prm[kArnMaxNV] in + sum_i prm[i] p_i (the
 // coefficients the control kernel wrote); nothing when the step was handed back (prm halt entry).
 hipError_t combo_prm_launch(double* out, const double* in, const double* prm, const VecList& P,
@@ -171,8 +179,8 @@ constexpr int kArnMaxNV = 35;
 // non-temporal load away from L2): ~9 % of the launch (profiles/r02_arnoldi_ab.md).  An edge
 // array holds, per group boundary b (column B = kEdgeW b) and row q, the four values
 // v[q][B-2], v[q][B-1], v[q][B], v[q][B+1] (columns mod nx): E[(b ny + q) 4 + 0..3], so four
-// consecutive rows share a line.  The fused kernel writes the edge arrays of its two outputs;
-// other producers of update entries run edge_gather_launch.
+// consecutive rows share a line.  The fused kernel, the stencil passes and the combinations
+// (EdgeOut) write the edge arrays of their outputs; other producers run edge_gather_launch.
 constexpr int kEdgeW = 256;
 __host__ __device__ inline int64_t edge_groups(int64_t nx) { return (nx + kEdgeW - 1) / kEdgeW; }
 __host__ __device__ inline int64_t edge_elems(int64_t ny, int64_t nx) { return edge_groups(nx) * ny * 4; }

@@ -258,6 +258,16 @@ int Engine::gather_edges(const double* v) {
                 [&] { return edge_gather_launch(v, e, edge_ny_, edge_nx_, s); });
 }
 
+EdgeOut Engine::edge_out(const double* v) {
+  EdgeOut eo;
+  eo.E = edges(v);
+  if (!eo.E) return eo;
+  mark_edges(v);
+  eo.nx = edge_nx_;
+  eo.ny = edge_ny_;
+  return eo;
+}
+
 hipEvent_t Engine::ev() {
   if (!free_ev_.empty()) {
     hipEvent_t e = free_ev_.back();

@@ -94,6 +94,9 @@ class Engine {
   bool edges_kept(const double* v) const;
   // Refresh the edge array of pool vector v from v (no-op without one).
   int gather_edges(const double* v);
+  // The edge array a combination writing pool vector v fills in place of gather_edges (marked
+  // kept; E == nullptr when v has none).
+  EdgeOut edge_out(const double* v);
   // Vector stride in the pool.  Large vectors get an odd multiple of 128 KiB: consecutive basis
   // vectors read at the same offset then spread over the HBM channels instead of landing on the
   // same ones (scripts/micro/march_bench.hip, 24 vectors of 4096^2 streamed row by row: pool
@@ -263,7 +266,10 @@ struct Problem {
   // v (a pool vector) may enter the update of a later fused step: refresh its edge array.
   // eval()'s F and jvp()'s w come with fresh edge arrays (written by the pass itself); the solver
   // calls this after the other producers of update entries (its in-place combinations).
-  virtual int publish_edges(const double* /*v*/) { return NK_OK; }
+  // written: the combination already wrote v's edge array (edge_out), only the rest is left.
+  virtual int publish_edges(const double* /*v*/, bool /*written*/ = false) { return NK_OK; }
+  // The edge array a combination that writes v should write itself (EdgeOut{}: none).
+  virtual EdgeOut edge_out(const double* /*v*/) { return EdgeOut{}; }
   // The last `count` fused steps were no-ops (queued past a step the device control handed
   // back): take their launches out of the kernel profile (Engine::void_last).
   virtual void void_fused_steps(int /*count*/) {}

@@ -600,10 +600,16 @@ void SHProblem::side_edges(StencilArgs* A, const double* a, const double* b) con
   if (b && E_.edges_kept(b)) A->Eb = E_.edges(b);
 }
 
-int SHProblem::publish_edges(const double* v) {
+int SHProblem::publish_edges(const double* v, bool written) {
   if (!has_fused(1)) return NK_OK;
-  const int rc = E_.gather_edges(v);
+  const int rc = written ? NK_OK : E_.gather_edges(v);
   return rc ? rc : push(v);
+}
+
+EdgeOut SHProblem::edge_out(const double* v) {
+  const char* e = std::getenv("NKHIP_COMBO_EDGES");  // 0: an edge_gather pass after each
+  if (!has_fused(1) || (e && e[0] == '0')) return EdgeOut{};
+  return E_.edge_out(v);
 }
 
 // ============================================================================================

@@ -33,7 +33,8 @@ class SHProblem final : public Problem {
                  const ArnTail* tail = nullptr, bool* tail_used = nullptr) override;
   int set_x0(const double* x0) override;
   int set_dir(const double* d) override;
-  int publish_edges(const double* v) override;
+  int publish_edges(const double* v, bool written = false) override;
+  EdgeOut edge_out(const double* v) override;
   void set_edges(StencilArgs* A, const double* out);
   void side_edges(StencilArgs* A, const double* a, const double* b) const;
   void void_fused_steps(int count) override;

@@ -207,6 +207,20 @@ def test_edges_identical_solve(ny, nx, monkeypatch):
     assert pb["arnoldi_fused"]["launches"] > 0
 
 
+@pytest.mark.parametrize("ny,nx", [(64, 600), (128, 512)])
+def test_combo_edges_identical_solve(ny, nx, monkeypatch):
+    """The LGMRES combinations write their outputs' edge arrays themselves (EdgeOut): the same
+    solve, bitwise, as with an edge_gather pass after each (NKHIP_COMBO_EDGES=0), and no
+    edge_gather launch is left.  nx = 600 puts the last group border at the row end."""
+    monkeypatch.setenv("NKHIP_COMBO_EDGES", "0")
+    _, a, sa, pa = _step(ny, nx, fused=True)
+    monkeypatch.delenv("NKHIP_COMBO_EDGES")
+    _, b, sb, pb = _step(ny, nx, fused=True)
+    assert np.array_equal(a, b) and sa == sb
+    assert pa.get("edge_gather", {}).get("launches", 0) > 0
+    assert pb.get("edge_gather", {}).get("launches", 0) == 0
+
+
 @pytest.mark.parametrize("ny,nx,fused", [(64, 64, True), (61, 61, False), (256, 256, True),
                                          (128, 600, True), (96, 130, False)])
 def test_speculative_jvp_identical(ny, nx, fused, monkeypatch):

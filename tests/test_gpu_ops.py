@@ -182,11 +182,12 @@ def test_config2_1024(op):
 
 
 @pytest.mark.parametrize("op", ["lap5", "sh13"])
-@pytest.mark.parametrize("ny,nx", [(2048, 1024), (2056, 1024), (6, 8), (3, 10)])
+@pytest.mark.parametrize("ny,nx", [(2048, 1024), (2056, 1024), (6, 8), (3, 10), (7, 700), (5, 258)])
 def test_tile_and_march_operators(op, ny, nx):
     """The pure operators take the one-row-per-thread tile kernel up to 2^21 points (config 2's
     1024^2) and the march kernel above: both against the oracle stencils on either side of the
-    switch (2048 x 1024 = 2^21: tile; 2056 x 1024: march) and on the smallest grids."""
+    switch (2048 x 1024 = 2^21: tile; 2056 x 1024: march), on the smallest grids and on rows that
+    end inside a wave (700, 258 columns: the lane exchange's row-end lanes load their own)."""
     import nkhip
     h, r = 0.625, 0.01
     v_np = np.random.default_rng(ny + nx).standard_normal(ny * nx)
