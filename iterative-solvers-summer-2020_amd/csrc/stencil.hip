@@ -437,53 +437,28 @@ __global__ void __launch_bounds__(256) point_kernel(StencilArgs A) {
 // (input and output) stays in its 4 MB L2 between back-to-back launches.  Same neighbour sums in
 // the same order as the march kernel: bitwise its results.
 // ------------------------------------------------------------------------------------------
-// XCH: a lane loads only its own column pair and takes its neighbours' from the adjacent lanes
-// (DPP wave shifts); lanes at a wave's ends or the row's ends load theirs.
-__device__ __forceinline__ double lane_up(double x) {  // lane i <- lane i-1 (0 at lane 0)
-  const uint2 b = __builtin_bit_cast(uint2, x);
-  return __builtin_bit_cast(double, make_uint2(__builtin_amdgcn_update_dpp(0u, b.x, 0x138, 0xF, 0xF, false),
-                                               __builtin_amdgcn_update_dpp(0u, b.y, 0x138, 0xF, 0xF, false)));
-}
-__device__ __forceinline__ double lane_down(double x) {  // lane i <- lane i+1 (0 at lane 63)
-  const uint2 b = __builtin_bit_cast(uint2, x);
-  return __builtin_bit_cast(double, make_uint2(__builtin_amdgcn_update_dpp(0u, b.x, 0x130, 0xF, 0xF, false),
-                                               __builtin_amdgcn_update_dpp(0u, b.y, 0x130, 0xF, 0xF, false)));
-}
-
-template <SMode M, int ROWS, bool NTS, bool XCH>
+template <SMode M, int ROWS, bool NTS>
 __global__ void __launch_bounds__(256) tile_kernel(StencilArgs A, int gxt) {
   constexpr int R = kRad<M>;
   constexpr int NR = 2 * R + ROWS;  // window rows of ROWS output rows
   const int64_t nx = A.nx, ny = A.ny;
   const int64_t lb = (int64_t(blockIdx.x) % 8) * (int64_t(gridDim.x) / 8) + blockIdx.x / 8;
   const int64_t nrb = (ny + ROWS - 1) / ROWS;
-  if (lb >= int64_t(gxt) * nrb) return;  // padding of the grid to a multiple of 8 (whole blocks)
+  if (lb >= int64_t(gxt) * nrb) return;  // padding of the grid to a multiple of 8
   const int64_t r0 = (lb / gxt) * ROWS;
-  const int64_t cl = 2 * ((lb % gxt) * 256 + threadIdx.x);
-  const bool act = cl < nx;
-  if (!XCH && !act) return;  // (XCH: every lane stays for the exchange; the idle ones store nothing)
-  const int64_t c0 = act ? cl : nx - 2;
+  const int64_t c0 = 2 * ((lb % gxt) * 256 + threadIdx.x);
+  if (c0 >= nx) return;
   const int64_t cm = (c0 >= 2) ? c0 - 2 : c0 - 2 + nx;
   const int64_t cp = (c0 + 2 < nx) ? c0 + 2 : c0 + 2 - nx;
-  const int lane = threadIdx.x & 63;
-  const bool own_l = lane == 0 || c0 == 0, own_r = lane == 63 || c0 + 2 >= nx;
   double w[NR][6];
 #pragma unroll
   for (int m = 0; m < NR; ++m) {
     int64_t rr = r0 + m - R;
     rr = (rr > ny + 1) ? ny + 1 : rr;  // rows past a short last block: a valid (halo) row
     const double* p = rowp_fast(A.a, rr, ny, nx);
+    const double2 x0 = *reinterpret_cast<const double2*>(p + cm);
     const double2 x1 = *reinterpret_cast<const double2*>(p + c0);
-    double2 x0, x2;
-    if constexpr (XCH) {
-      x0 = make_double2(lane_up(x1.x), lane_up(x1.y));
-      x2 = make_double2(lane_down(x1.x), lane_down(x1.y));
-      if (own_l) x0 = *reinterpret_cast<const double2*>(p + cm);
-      if (own_r) x2 = *reinterpret_cast<const double2*>(p + cp);
-    } else {
-      x0 = *reinterpret_cast<const double2*>(p + cm);
-      x2 = *reinterpret_cast<const double2*>(p + cp);
-    }
+    const double2 x2 = *reinterpret_cast<const double2*>(p + cp);
     w[m][0] = x0.x; w[m][1] = x0.y; w[m][2] = x1.x; w[m][3] = x1.y; w[m][4] = x2.x; w[m][5] = x2.y;
   }
 #pragma unroll
@@ -505,7 +480,7 @@ __global__ void __launch_bounds__(256) tile_kernel(StencilArgs A, int gxt) {
       }
       res[q] = finish<M>(A, na, nb, 0.0, 0.0, 1.0);
     }
-    if (r0 + t < ny && act) {
+    if (r0 + t < ny) {
       dv2* o = reinterpret_cast<dv2*>(A.out0 + (r0 + t) * nx + c0);
       const dv2 v{res[0].o0, res[1].o0};
       if constexpr (NTS)
@@ -548,26 +523,20 @@ hipError_t launch_mode(const StencilArgs& A, hipStream_t s, int64_t* nblk) {
         // rows per thread and the store policy (NKHIP_TILE_ROWS 1 / 2 / 4, NKHIP_TILE_NT): at
         // 1024^2, rocprofv3, one box (profiles/r05_config2.md): march 6.43 us; rows 1 / 2 / 4
         // 5.93 / 5.13 / 5.21 us with plain stores, 5.18-5.41 / 4.83 / 4.80-4.86 us non-temporal
-        // NKHIP_TILE_XCH: neighbour columns by lane exchange instead of two more loads per row
         static const int rows = env_int("NKHIP_TILE_ROWS", 2);
         static const bool nts = env_int("NKHIP_TILE_NT", 1) != 0;
-        static const bool xch = env_int("NKHIP_TILE_XCH", 0) != 0;
         const int rt = (rows == 4 || rows == 2) ? rows : 1;
         const int gxt = int((A.nx / 2 + 255) / 256);
         const int64_t nb = int64_t(gxt) * ((A.ny + rt - 1) / rt);
         if (nblk) *nblk = nb;
         const dim3 grid{unsigned((nb + 7) / 8 * 8), 1u, 1u};
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, gxt); };
-        if (xch && rt == 4)
-          nts ? go(tile_kernel<M, 4, true, true>) : go(tile_kernel<M, 4, false, true>);
-        else if (xch)
-          nts ? go(tile_kernel<M, 2, true, true>) : go(tile_kernel<M, 2, false, true>);
-        else if (rt == 4)
-          nts ? go(tile_kernel<M, 4, true, false>) : go(tile_kernel<M, 4, false, false>);
+        if (rt == 4)
+          nts ? go(tile_kernel<M, 4, true>) : go(tile_kernel<M, 4, false>);
         else if (rt == 2)
-          nts ? go(tile_kernel<M, 2, true, false>) : go(tile_kernel<M, 2, false, false>);
+          nts ? go(tile_kernel<M, 2, true>) : go(tile_kernel<M, 2, false>);
         else
-          nts ? go(tile_kernel<M, 1, true, false>) : go(tile_kernel<M, 1, false, false>);
+          nts ? go(tile_kernel<M, 1, true>) : go(tile_kernel<M, 1, false>);
         return hipGetLastError();
       }
     }
