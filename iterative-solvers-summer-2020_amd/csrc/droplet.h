@@ -98,14 +98,17 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
                              const double* prm = nullptr);
 
 // Device tables of the PMA solve (solve_PMA, :578-587): orthonormal DCT-II matrices Cx (nx*nx),
-// Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the four DCT operands of the MFMA path in
-// v_mfma_f64_16x16x4 fragment order (zero-padded to 16-row/column tiles and 4-deep k steps):
-//   fa1: A = Cy     (T1 = Cy X)      fb2: B = Cx^T (T2 = T1 Cx^T)
-//   fa3: A = Cy^T   (Y1 = Cy^T T2)   fb4: B = Cx   (dQ = Y1 Cx)
-// A fragments: [mt][s][lane] = A[16mt + (lane&15)][4s + (lane>>4)];
-// B fragments: [nt][s][lane] = B[4s + (lane>>4)][16nt + (lane&15)].
+// Cy (ny*ny), den = 1 - gamma*Leig (ny*nx), and the operands of the four DCT products of the
+// MFMA path with the transform's first butterfly folded in (droplet.hip dct_pair), in
+// v_mfma_f64_16x16x4 fragment order (zero-padded to 16-wide tiles and 4-deep k steps), half
+// index h < ceil(N/2), N the transformed length, C its DCT-II matrix:
+//   f[0]: A = even / odd rows of Cy (T1 = Cy X)     f[1]: B, the same of Cx (T2 = T1 Cx^T)
+//   f[2]: A = Cy^T by even / odd frequency (Y1)     f[3]: B, the same of Cx (dQ = Y1 Cx)
+// f[g][0] even part, f[g][1] odd part.  A fragments: [t][s][lane] = A[16t + (lane&15)][4s +
+// (lane>>4)]; B fragments: [t][s][lane] = B[4s + (lane>>4)][16t + (lane&15)].
 struct PmaTables {
-  const double *cx, *cy, *den, *fa1, *fb2, *fa3, *fb4;
+  const double *cx, *cy, *den;
+  const double* f[4][2];
 };
 size_t drop_pma_table_size(const DropParams& P);
 std::vector<double> drop_pma_tables(const DropParams& P);

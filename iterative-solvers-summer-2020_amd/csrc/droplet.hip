@@ -190,6 +190,22 @@ struct FastDiv {
   __device__ int operator()(int t) const { return int(__umulhi(uint32_t(t), m)); }
 };
 
+// point u of the boundary ring: rows 0-2 and ny-3..ny-1, then columns 0-2 and nx-3..nx-1 of
+// rows 3..ny-4
+__device__ __forceinline__ void ring_point(int u, int nx, int ny, const FastDiv& diy,
+                                           const FastDiv& dnx, int* i, int* j) {
+  if (u < 6 * nx) {
+    const int r = dnx(u);
+    *i = r < 3 ? r : ny - 6 + r;
+    *j = u - r * nx;
+  } else {
+    u -= 6 * nx;
+    const int c = diy(u);
+    *j = c < 3 ? c : nx - 6 + c;
+    *i = 3 + (u - c * (ny - 6));
+  }
+}
+
 template <class F>
 __device__ __forceinline__ void for_points(int nx, int ny, F f) {
   const int ix = nx - 6, iy = ny - 6, nI = ix * iy, NN = nx * ny;
@@ -200,17 +216,8 @@ __device__ __forceinline__ void for_points(int nx, int ny, F f) {
       const int i = 3 + q, j = 3 + (t - q * ix);
       f(i * nx + j, i, j, std::true_type{});
     } else {
-      int u = t - nI, i, j;
-      if (u < 6 * nx) {  // rows 0-2 and ny-3..ny-1
-        const int r = dnx(u);
-        i = r < 3 ? r : ny - 6 + r;
-        j = u - r * nx;
-      } else {  // columns 0-2 and nx-3..nx-1 of rows 3..ny-4
-        u -= 6 * nx;
-        const int c = diy(u);
-        j = c < 3 ? c : nx - 6 + c;
-        i = 3 + (u - c * iy);
-      }
+      int i, j;
+      ring_point(t - nI, nx, ny, diy, dnx, &i, &j);
       f(i * nx + j, i, j, std::false_type{});
     }
   }
@@ -218,52 +225,117 @@ __device__ __forceinline__ void for_points(int nx, int ny, F f) {
 #define FOR_POINTS(NN) \
   for_points(nx, ny, [&](const int p_, const int i_, const int j_, auto kin_)
 
+// The stencil stages visit the interior in column strips instead: a thread takes one column j
+// and kS consecutive rows i0 .. i0+kS-1 (one pass over the droplet's 85 x 55 interior with 935
+// threads), loads the neighbours its points share once into registers -- the strip's window --
+// and computes every point from them with the same operators in the same summation order as the
+// point walk (a register array indexed by constants is what op1 / lap_axis read then).  All of a
+// strip's loads precede its stores, so they issue together; then the boundary ring point-wise.
+constexpr int kS = 5;
+
+template <class F>
+__device__ __forceinline__ void for_strips(int nx, int ny, F f) {
+  const int ix = nx - 6, iy = ny - 6, ns = (iy + kS - 1) / kS;
+  const FastDiv dix(ix);
+  for (int t = threadIdx.x; t < ns * ix; t += DB) {
+    const int s = dix(t);
+    f(3 + kS * s, 3 + (t - s * ix), min(kS, iy - kS * s));  // (i0, j, rows of this strip)
+  }
+}
+
+template <class F>
+__device__ __forceinline__ void for_ring(int nx, int ny, F f) {
+  const int nR = nx * ny - (nx - 6) * (ny - 6);
+  const FastDiv diy(ny - 6), dnx(nx);
+  for (int u = threadIdx.x; u < nR; u += DB) {
+    int i, j;
+    ring_point(u, nx, ny, diy, dnx, &i, &j);
+    f(i * nx + j, i, j);
+  }
+}
+
+// W[r][c] = v(i0 - R + r, j - CW + c): rows clamped to the grid (a short last strip computes
+// rows it does not store); entries a stage never reads are dead loads the compiler drops
+template <int R, int CW, int NR = kS + 2 * R>
+__device__ __forceinline__ void load_window(double (&W)[NR][2 * CW + 1], const double* v, int ld,
+                                            int i0, int j, int ny) {
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int row = min(i0 - R + r, ny - 1);
+#pragma unroll
+    for (int c = 0; c <= 2 * CW; ++c) W[r][c] = v[row * ld + j - CW + c];
+  }
+}
+
 // ---------------------------------------------------------------------------- kernels
+// compute_Q_spatial_ders (:696-711), J (:376) and the Laplace metric (:612-614) at grid point
+// (i, j), reading q at (iq, jq) of a field with row stride ldq: the grid plane itself (iq, jq =
+// i, j) or, in the interior (kIn), a strip's register window
+struct MeshPt {
+  double qd, qe, q2x, q2y, qxy, J, A11, A22, A12;
+};
+template <bool kIn>
+__device__ __forceinline__ MeshPt mesh_point(const DropParams& P, const Coefs& C, const double* q,
+                                             int ldq, int iq, int jq, int i, int j) {
+  const int nx = P.nx, ny = P.ny;
+  const bool left = !kIn && j == 0, right = !kIn && j == nx - 1;
+  const bool bottom = !kIn && i == 0, top = !kIn && i == ny - 1;
+  MeshPt m;
+  m.qd = dx1<kIn>(C, q, iq, jq, nx, ldq);
+  m.qe = dy1<kIn>(C, q, iq, jq, ny, ldq);
+  if (left) m.qd = P.endl;
+  if (right) m.qd = P.endr;
+  if (bottom) m.qe = P.endb;
+  if (top) m.qe = P.endt;
+  double t = 0.0;
+  if (left) t = 25 / (6 * P.dksi) * fabs(P.endl);
+  if (right) t = 25 / (6 * P.dksi) * fabs(P.endr);
+  m.q2x = op1<2, kIn>(C, q + iq * ldq, jq, nx, 1) + t;
+  t = 0.0;
+  if (top) t = 25 / (6 * P.deta) * fabs(P.endt);
+  if (bottom) t = 25 / (6 * P.deta) * fabs(P.endb);
+  m.q2y = op1<3, kIn>(C, q + jq, iq, ny, ldq) + t;
+  m.qxy = (left || right || top || bottom) ? 0.0 : dxy<kIn>(C, q, iq, jq, nx, ny, ldq);
+  m.J = m.q2x * m.q2y - m.qxy * m.qxy;
+  m.A11 = (m.qxy * m.qxy + m.q2y * m.q2y) / m.J;
+  m.A22 = (m.qxy * m.qxy + m.q2x * m.q2x) / m.J;
+  m.A12 = -(m.qxy * (m.q2x + m.q2y)) / m.J;
+  return m;
+}
+
 // all == false: only the fields the PMA iteration itself reads next (J, A12; A11 / A22 go to the
 // LDS planes) -- the loop's last iteration writes the full set the caller reads afterwards
 __device__ void mesh_stage(const DropParams& P, const Coefs& C, const double* q, int ldq,
                            const DropMesh& M, double* a11 = nullptr, double* a22 = nullptr,
                            bool all = true) {
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  // compute_Q_spatial_ders (:696-711), J (:376) and the Laplace metric (:612-614): point-wise
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int p = p_, i = i_, j = j_;
-    const bool left = j == 0, right = j == nx - 1, bottom = i == 0, top = i == ny - 1;
-    double qd = dx1<kIn>(C, q, i, j, nx, ldq), qe = dy1<kIn>(C, q, i, j, ny, ldq);
-    if (left) qd = P.endl;
-    if (right) qd = P.endr;
-    if (bottom) qe = P.endb;
-    if (top) qe = P.endt;
-    double t = 0.0;
-    if (left) t = 25 / (6 * P.dksi) * fabs(P.endl);
-    if (right) t = 25 / (6 * P.dksi) * fabs(P.endr);
-    const double q2x = op1<2, kIn>(C, q + i * ldq, j, nx, 1) + t;
-    t = 0.0;
-    if (top) t = 25 / (6 * P.deta) * fabs(P.endt);
-    if (bottom) t = 25 / (6 * P.deta) * fabs(P.endb);
-    const double q2y = op1<3, kIn>(C, q + j, i, ny, ldq) + t;
-    const double qxy = (left || right || top || bottom) ? 0.0 : dxy<kIn>(C, q, i, j, nx, ny, ldq);
-    const double J = q2x * q2y - qxy * qxy;
+  const int nx = P.nx, ny = P.ny;
+  auto put = [&](int p, int i, int j, const MeshPt& m) {
     if (all) {
-      M.dksi[p] = qd;
-      M.deta[p] = qe;
-      M.d2ksi[p] = q2x;
-      M.d2eta[p] = q2y;
-      M.dksideta[p] = qxy;
+      M.dksi[p] = m.qd;
+      M.deta[p] = m.qe;
+      M.d2ksi[p] = m.q2x;
+      M.d2eta[p] = m.q2y;
+      M.dksideta[p] = m.qxy;
     }
-    M.J[p] = J;
-    const double A11 = (qxy * qxy + q2y * q2y) / J, A22 = (qxy * qxy + q2x * q2x) / J;
+    M.J[p] = m.J;
     if (all) {
-      M.A11[p] = A11;
-      M.A22[p] = A22;
+      M.A11[p] = m.A11;
+      M.A22[p] = m.A22;
     }
     if (a11) {
-      a11[i * ldq + j] = A11;
-      a22[i * ldq + j] = A22;
+      a11[i * ldq + j] = m.A11;
+      a22[i * ldq + j] = m.A22;
     }
-    M.A12[p] = -(qxy * (q2x + q2y)) / J;
+    M.A12[p] = m.A12;
+  };
+  for_strips(nx, ny, [&](int i0, int j, int nr) {  // the 5 x 5 neighbourhood of each point
+    double W[kS + 4][5];
+    load_window<2, 2>(W, q, ldq, i0, j, ny);
+#pragma unroll
+    for (int s = 0; s < kS; ++s)
+      if (s < nr) put((i0 + s) * nx + j, i0 + s, j, mesh_point<true>(P, C, &W[0][0], 5, s + 2, 2, 0, 0));
   });
+  for_ring(nx, ny, [&](int p, int i, int j) { put(p, i, j, mesh_point<false>(P, C, q, ldq, i, j, i, j)); });
 }
 
 __global__ void __launch_bounds__(DB) drop_mesh_kernel(DropParams P, Coefs Ck, const double* q,
@@ -303,9 +375,26 @@ template <bool kRaw = false>
 __device__ void uders_stage(const DropParams& P, const Coefs& C, const DropMesh& M, CPlane u,
                             Plane t1, Plane t2) {
   const int nx = P.nx, ny = P.ny;
-  for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
-    constexpr bool kIn = decltype(kin)::value;
-    double ud = dx1<kIn>(C, u, i, j, nx), ue = dy1<kIn>(C, u, i, j, ny);
+  for_strips(nx, ny, [&](int i0, int j, int nr) {  // interior: no boundary rules
+    double W[kS + 4][5];  // (the cross of each point's 5 x 5 neighbourhood is read)
+    load_window<2, 2>(W, u.v, u.ld, i0, j, ny);
+    double ud[kS], ue[kS], a[kS];
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+      ud[s] = dx1<true>(C, &W[0][0], s + 2, 2, nx, 5);
+      ue[s] = dy1<true>(C, &W[0][0], s + 2, 2, ny, 5);
+      a[s] = M.A12[min(i0 + s, ny - 1) * nx + j];
+    }
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+      if (s < nr) {
+        t1(i0 + s, j) = a[s] * ue[s];
+        t2(i0 + s, j) = a[s] * ud[s];
+      }
+    }
+  });
+  for_ring(nx, ny, [&](const int p, const int i, const int j) {
+    double ud = dx1<false>(C, u, i, j, nx), ue = dy1<false>(C, u, i, j, ny);
     if (!kRaw) {
       if (j == 0 || j == nx - 1) ud = 0.0;
       if (i == ny - 1) ue = 0.0;
@@ -602,17 +691,37 @@ __global__ void __launch_bounds__(DB) mems_resid_kernel(DropParams P, Coefs Ck, 
 // matrices (91x91 and 61x61 at the reference size).
 
 // One pass of the 9-point monitor filter (:740-756), T -> Mo, both with row stride ld.
-__device__ void smooth_pass(const DropParams& P, const double* T, double* Mo, int ld) {
-  const int nx = P.nx, ny = P.ny, NN = nx * ny;
-  FOR_POINTS(NN) {
-    [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
-    const int i = i_, j = j_;
-    auto t = [&](int a, int b) { return T[a * ld + b]; };
+template <class Tf>
+__device__ __forceinline__ double smooth9(Tf t, int i, int j) {
+  return t(i, j) + (t(i - 1, j) + t(i + 1, j) + t(i, j - 1) + t(i, j + 1)) / 8 +
+         (t(i - 1, j - 1) + t(i - 1, j + 1) + t(i + 1, j - 1) + t(i + 1, j + 1)) / 16;
+}
+// T has row stride ldt, Mo ldm.  J (optional): also return this thread's share of the Mackenzie
+// integral sum(Mo |J|) (:757-759) over the points it wrote.
+__device__ double smooth_pass(const DropParams& P, const double* T, int ldt, double* Mo, int ldm,
+                              const double* J = nullptr) {
+  const int nx = P.nx, ny = P.ny;
+  double acc = 0.0;
+  for_strips(nx, ny, [&](int i0, int j, int nr) {
+    double W[kS + 2][3];
+    load_window<1, 1>(W, T, ldt, i0, j, ny);
+    double v[kS];
+#pragma unroll
+    for (int s = 0; s < kS; ++s) v[s] = smooth9([&](int a, int b) { return W[a][b]; }, s + 1, 1);
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+      if (s < nr) {
+        Mo[(i0 + s) * ldm + j] = v[s];
+        if (J) acc += v[s] * fabs(J[(i0 + s) * nx + j]);
+      }
+    }
+  });
+  for_ring(nx, ny, [&](const int p, const int i, const int j) {
+    auto t = [&](int a, int b) { return T[a * ldt + b]; };
     double v;
     const bool in_i = i > 0 && i < ny - 1, in_j = j > 0 && j < nx - 1;
-    if (kIn || (in_i && in_j)) {
-      v = t(i, j) + (t(i - 1, j) + t(i + 1, j) + t(i, j - 1) + t(i, j + 1)) / 8 +
-          (t(i - 1, j - 1) + t(i - 1, j + 1) + t(i + 1, j - 1) + t(i + 1, j + 1)) / 16;
+    if (in_i && in_j) {
+      v = smooth9(t, i, j);
     } else if (in_i && j == nx - 1) {
       v = (4 * t(i, j) + 2 * t(i - 1, j) + 2 * t(i + 1, j) + 2 * t(i, j - 1) + t(i + 1, j - 1) +
            t(i - 1, j - 1)) / 12;
@@ -634,8 +743,10 @@ __device__ void smooth_pass(const DropParams& P, const double* T, double* Mo, in
     } else {
       v = (4 * t(i, j) + 2 * t(i, j - 1) + 2 * t(i - 1, j) + t(i - 1, j - 1)) / 9;
     }
-    Mo[i * ld + j] = v;
+    Mo[i * ldm + j] = v;
+    if (J) acc += v * fabs(J[p]);
   });
+  return acc;
 }
 
 // Mackenzie regularisation integral sum(mon |J|) dksi deta (:757-759), broadcast to all threads.
@@ -686,7 +797,7 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
     double* T = S.ud;
     double* Mo = S.ue;
     for (int sm = 0; sm < P.smoothing_iters; ++sm) {
-      smooth_pass(P, T, Mo, nx);
+      smooth_pass(P, T, nx, Mo, nx);
       __syncthreads();
       double* sw = T;
       T = Mo;
@@ -752,54 +863,71 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// out(m, n) = sum_{k<K} A(m, k) B(k, n), m < M, n < N.
-// kConstA: A from fragment table `frag`, B(k, n) = plane[k*ld + n]; a wave task is 16 x 32.
-// else:    B from fragment table `frag`, A(m, k) = plane[m*ld + k]; a wave task is 32 x 16.
-// Padded k (>= K) has zero fragment entries; the plane index is clamped so it reads finite data.
-template <bool kConstA, class Fn>
-__device__ __forceinline__ void dct_mfma(const double* __restrict__ frag, const double* plane,
-                                         int ld, int K, int M, int N, Fn f) {
+// The DCT products with the transform's first butterfly folded in: DCT-II rows are even or odd
+// about the middle (C[k][N-1-n] = (-1)^k C[k][n]), so
+//   forward (kInv false): frequency 2h takes s_k = x_k + x_{N-1-k}, frequency 2h+1 takes
+//     d_k = x_k - x_{N-1-k}, k < ceil(N/2) (an odd N's middle entry: weight C/2 on s = 2 x_mid);
+//   inverse (DCT-III): E_h, O_h sum the even / odd frequencies, h < ceil(N/2), and
+//     y_h = E_h + O_h, y_{N-1-h} = E_h - O_h.
+// Half the multiply-adds of the dense product.  A wave task is the even and the odd 16 x 16 tile
+// of one half-index range: each loaded operand pair feeds both (forward), each E / O pair meets in
+// one epilogue (inverse).  f(t, o, value): t the transformed index, o the other one.
+// kConstA: transform along rows (A = table [h][k], B(k, o) = plane[k*ld + o], o < No);
+// else along columns (A(o, k) = plane[o*ld + k], o < No, B = table [k][h]).
+// Padded k steps have zero table entries; plane indices are clamped so they read finite data.
+template <bool kConstA, bool kInv, class Fn>
+__device__ __forceinline__ void dct_pair(const double* __restrict__ fe,
+                                         const double* __restrict__ fo, const double* plane,
+                                         int ld, int Nt, int No, Fn f) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int S = pma_ksteps(K), Mt = (M + 15) >> 4, Nt = (N + 15) >> 4;
-  const int tM = kConstA ? Mt : (Mt + 1) >> 1, tN = kConstA ? (Nt + 1) >> 1 : Nt;
-  for (int task = wave; task < tM * tN; task += kWaves) {
-    const int ti = task / tN, tj = task - ti * tN;
-    // tile origins: two tiles side by side (kConstA: along n; else along m)
-    const int m0 = kConstA ? 16 * ti : 32 * ti, n0 = kConstA ? 32 * tj : 16 * tj;
-    const double* fr = frag + size_t(kConstA ? ti : tj) * S * 64 + lane;
-    f64x4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = {0.0, 0.0, 0.0, 0.0};
-    // operands of kBatch k steps are loaded together, then their MFMAs issue: one memory
-    // round trip per batch instead of per step (steps past S are skipped, uniformly)
-    const double* p0 = kConstA ? plane + min(n0 + r, N - 1) : plane + min(m0 + r, M - 1) * ld;
-    const double* p1 =
-        kConstA ? plane + min(n0 + 16 + r, N - 1) : plane + min(m0 + 16 + r, M - 1) * ld;
-    const int kstride = kConstA ? ld : 1;
+  const int hs = (Nt + 1) >> 1, S = pma_ksteps(hs), Ht = (hs + 15) >> 4, Ot = (No + 15) >> 4;
+  for (int task = wave; task < Ht * Ot; task += kWaves) {
+    const int th = task / Ot, to = task - th * Ot;
+    const int h0 = 16 * th, o0 = 16 * to;
+    const double* pe = fe + size_t(th) * S * 64 + lane;
+    const double* po = fo + size_t(th) * S * 64 + lane;
+    const int oc = min(o0 + r, No - 1);  // this lane's plane line (column or row), clamped
+    const double* pl = kConstA ? plane + oc : plane + oc * ld;
+    const int ks = kConstA ? ld : 1;
+    f64x4 ce = {0.0, 0.0, 0.0, 0.0}, co = {0.0, 0.0, 0.0, 0.0};
     for (int s0 = 0; s0 < S; s0 += kBatch) {  // S is a multiple of kBatch (zero-padded)
-      double fv[kBatch], x0[kBatch], x1[kBatch];
+      double ve[kBatch], vo[kBatch], xe[kBatch], xo[kBatch];
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
-        const int k = min(4 * (s0 + u) + g, K - 1);
-        fv[u] = fr[(s0 + u) * 64];
-        x0[u] = p0[k * kstride];
-        x1[u] = p1[k * kstride];
+        const int k = 4 * (s0 + u) + g;
+        ve[u] = pe[(s0 + u) * 64];
+        vo[u] = po[(s0 + u) * 64];
+        if (kInv) {
+          xe[u] = pl[min(2 * k, Nt - 1) * ks];
+          xo[u] = pl[min(2 * k + 1, Nt - 1) * ks];
+        } else {
+          const int kc = min(k, hs - 1);
+          const double a = pl[kc * ks], b = pl[(Nt - 1 - kc) * ks];
+          xe[u] = a + b;
+          xo[u] = a - b;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
-        c0 = kConstA ? mfma_f64(fv[u], x0[u], c0) : mfma_f64(x0[u], fv[u], c0);
-        c1 = kConstA ? mfma_f64(fv[u], x1[u], c1) : mfma_f64(x1[u], fv[u], c1);
+        ce = kConstA ? mfma_f64(ve[u], xe[u], ce) : mfma_f64(xe[u], ve[u], ce);
+        co = kConstA ? mfma_f64(vo[u], xo[u], co) : mfma_f64(xo[u], vo[u], co);
       }
     }
-    // D layout: row = (lane >> 4) + 4*reg, col = lane & 15
+    // D layout: row = (lane >> 4) + 4*reg, col = lane & 15 (the half index runs along A's rows
+    // when kConstA, along B's columns otherwise)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int m = m0 + g + 4 * v, n = n0 + r;
-      if (kConstA) {
-        if (m < M && n < N) f(m, n, c0[v]);
-        if (m < M && n + 16 < N) f(m, n + 16, c1[v]);
-      } else {
-        if (m < M && n < N) f(m, n, c0[v]);
-        if (m + 16 < M && n < N) f(m + 16, n, c1[v]);
+      const int h = kConstA ? h0 + g + 4 * v : h0 + r;
+      const int o = kConstA ? o0 + r : o0 + g + 4 * v;
+      if (h < hs && o < No) {
+        if (kInv) {
+          f(h, o, ce[v] + co[v]);
+          if (Nt - 1 - h > h) f(Nt - 1 - h, o, ce[v] - co[v]);
+        } else {
+          f(2 * h, o, ce[v]);
+          if (2 * h + 1 < Nt) f(2 * h + 1, o, co[v]);
+        }
       }
     }
   }
@@ -807,10 +935,9 @@ __device__ __forceinline__ void dct_mfma(const double* __restrict__ frag, const 
 
 __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
     DropParams P, Coefs Ck, DropMesh M, DropScratch S, double* q, const double* uval,
-    const double* uxx0, const double* uyy0, const double* __restrict__ fa1,
-    const double* __restrict__ fb2, const double* __restrict__ fa3, const double* __restrict__ fb4,
-    const double* __restrict__ den, double dtm, int loops, int monitor,
+    const double* uxx0, const double* uyy0, PmaTables Tb, double dtm, int loops, int monitor,
     unsigned long long* tprof) {
+  const double* __restrict__ den = Tb.den;
   const Coefs& C = Ck;
   coef_rows_init(C);
   const int nx = P.nx, ny = P.ny, NN = nx * ny, ld = nx | 1;
@@ -820,7 +947,7 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
   double* L1 = L0 + ny * ld;
   double* L2 = L1 + ny * ld;
   // optional per-stage timing (NKHIP_PMA_TIMING): thread 0 accumulates wall-clock deltas
-  unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = 0;
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto mark = [&](int k) {
     if (tprof && threadIdx.x == 0) {
       const unsigned long long t = wall_clock64();
@@ -829,19 +956,17 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
     }
   };
   mark(-1);
+  // q of iterations > 0 is in L0 already: the previous iteration's last DCT product wrote it there
   for (int it = 0; it < loops; ++it) {
+    const double* T = L0;  // the monitor
     if (monitor == kMonGap) {
       if (it > 0) {  // the mesh fields (J) of the updated q
-        FOR_POINTS(NN) { L0[i_ * ld + j_] = q[p_]; });
-        __syncthreads();
         mesh_stage(P, C, L0, ld, M);
         __syncthreads();
       }
       FOR_POINTS(NN) { L0[i_ * ld + j_] = 1 / pow(1 + uval[p_], 6.0); });  // (PMA2_nk.py:357)
     } else if (it > 0) {
-      // compute_Q_spatial_ders + J (:595-596) from q staged in L0; A11 -> L1, A22 -> L2
-      FOR_POINTS(NN) { L0[i_ * ld + j_] = q[p_]; });
-      __syncthreads();
+      // compute_Q_spatial_ders + J (:595-596) from q in L0; A11 -> L1, A22 -> L2
       mesh_stage(P, C, L0, ld, M, L1, L2, it == loops - 1);
       __syncthreads();
       mark(0);
@@ -850,13 +975,16 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
       __syncthreads();
       uders_stage(P, C, M, CPlane(L0, ld), Plane{S.t1, nx}, Plane{S.t2, nx});
       __syncthreads();
-      // (u_xx / u_yy of the iteration's mesh are not read again: only the monitor is kept)
+      mark(1);
+      // (u_xx / u_yy of the iteration's mesh are not read again: only the monitor is kept, in
+      // global scratch while the three planes are busy, then in L0; reading it from there in
+      // the first smoothing pass instead costs more than the copy: 19.6 against 8.7 us)
       lap_pressure_stage(P, C, M, CPlane(L0, ld), CPlane(L1, ld), CPlane(L2, ld),
                          CPlane(S.t1, nx), CPlane(S.t2, nx), nullptr, nullptr, S.ud,
                          Plane{S.p, nx});
+      mark(2);
       __syncthreads();
       FOR_POINTS(NN) { L0[i_ * ld + j_] = S.ud[p_]; });
-      mark(1);
     } else {
       FOR_POINTS(NN) {
         const double s = fabs(uxx0[p_] + uyy0[p_]);  // monitor |u_xx + u_yy|^2 (:737)
@@ -864,42 +992,55 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
       });
     }
     __syncthreads();
-    double* T = L0;
-    double* Mo = L1;
+    // smoothing passes ping-pong L1 / L0 (an odd count ends in L1, an even one in L0); the last
+    // one also sums this thread's share of the Mackenzie integral
+    double part[1] = {0.0};
     for (int sm = 0; sm < P.smoothing_iters; ++sm) {
-      smooth_pass(P, T, Mo, ld);
+      double* Mo = (sm % 2 == 0) ? L1 : L0;
+      part[0] = smooth_pass(P, T, ld, Mo, ld, sm == P.smoothing_iters - 1 ? M.J : nullptr);
       __syncthreads();
-      double* sw = T;
       T = Mo;
-      Mo = sw;
     }
-    mark(2);
-    const double integral = monitor_integral(P, M, T, ld, &bcast);
+    mark(3);
+    if (P.smoothing_iters == 0) FOR_POINTS(NN) { part[0] += T[i_ * ld + j_] * fabs(M.J[p_]); });
+    // Mackenzie regularisation integral sum(mon |J|) dksi deta (:757-759)
+    {
+      const double tot = block_reduce<1, 1, DB>(part);
+      if (threadIdx.x == 0) bcast = tot * P.dksi * P.deta;
+      __syncthreads();
+    }
+    const double integral = bcast;
     // q_rhs = sqrt(mon |J|) / alpha (:584) -> L2
     FOR_POINTS(NN) {
     [[maybe_unused]] constexpr bool kIn = decltype(kin_)::value;
       L2[i_ * ld + j_] = sqrt((T[i_ * ld + j_] + P.C * integral) * fabs(M.J[p_])) / P.alpha;
     });
     __syncthreads();
-    mark(3);
+    mark(4);
     // DCT-II along eta: T1 = Cy X (L2 -> L0)
-    dct_mfma<true>(fa1, L2, ld, ny, ny, nx, [&](int m, int n, double v) { L0[m * ld + n] = v; });
+    dct_pair<true, false>(Tb.f[0][0], Tb.f[0][1], L2, ld, ny, nx,
+                          [&](int t, int o, double v) { L0[t * ld + o] = v; });
     __syncthreads();
     // along xi: T2 = T1 Cx^T, / (1 - gamma Leig) (:585-586) (L0 -> L1)
-    dct_mfma<false>(fb2, L0, ld, nx, ny, nx,
-                    [&](int m, int n, double v) { L1[m * ld + n] = v / den[m * nx + n]; });
+    dct_pair<false, false>(Tb.f[1][0], Tb.f[1][1], L0, ld, nx, ny,
+                           [&](int t, int o, double v) { L1[o * ld + t] = v / den[o * nx + t]; });
     __syncthreads();
     // inverse (DCT-III ortho) along eta: Y1 = Cy^T T2 (L1 -> L2)
-    dct_mfma<true>(fa3, L1, ld, ny, ny, nx, [&](int m, int n, double v) { L2[m * ld + n] = v; });
+    dct_pair<true, true>(Tb.f[2][0], Tb.f[2][1], L1, ld, ny, nx,
+                         [&](int t, int o, double v) { L2[t * ld + o] = v; });
     __syncthreads();
     // along xi: dQ = Y1 Cx; Q.val += dt * Q.dt (:587, :591, :599)
-    dct_mfma<false>(fb4, L2, ld, nx, ny, nx,
-                    [&](int m, int n, double v) { q[m * nx + n] = q[m * nx + n] + dtm * v; });
+    // (the new q also into L0, where the next iteration's mesh stage reads it)
+    dct_pair<false, true>(Tb.f[3][0], Tb.f[3][1], L2, ld, nx, ny, [&](int t, int o, double v) {
+      const double qn = q[o * nx + t] + dtm * v;
+      q[o * nx + t] = qn;
+      L0[o * ld + t] = qn;
+    });
     __syncthreads();
-    mark(4);
+    mark(5);
   }
   if (tprof && threadIdx.x == 0)
-    for (int k = 0; k < 5; ++k) tprof[k] = tacc[k];
+    for (int k = 0; k < 6; ++k) tprof[k] = tacc[k];
 }
 
 
@@ -1000,24 +1141,31 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
 // once per stepper.
 namespace {
 size_t frag_size(int tiles, int K) { return size_t(tiles) * pma_ksteps(K) * 64; }
+// the half length of product g's transformed axis (0, 2: eta = ny; 1, 3: xi = nx) and its tables
+int pma_half(const DropParams& P, int g) { return ((g % 2 ? P.nx : P.ny) + 1) / 2; }
+size_t pma_frag(const DropParams& P, int g) {
+  const int hs = pma_half(P, g);
+  return frag_size((hs + 15) / 16, hs);
+}
 }  // namespace
 
 size_t drop_pma_table_size(const DropParams& P) {
-  const int mt = (P.ny + 15) / 16, nt = (P.nx + 15) / 16;
-  return size_t(P.nx) * P.nx + size_t(P.ny) * P.ny + size_t(P.nx) * P.ny +
-         2 * frag_size(mt, P.ny) + 2 * frag_size(nt, P.nx);
+  size_t n = size_t(P.nx) * P.nx + size_t(P.ny) * P.ny + size_t(P.nx) * P.ny;
+  for (int g = 0; g < 4; ++g) n += 2 * pma_frag(P, g);
+  return n;
 }
 
 PmaTables drop_pma_view(const DropParams& P, const double* t) {
-  const int mt = (P.ny + 15) / 16, nt = (P.nx + 15) / 16;
   PmaTables T;
   T.cx = t;
   T.cy = T.cx + size_t(P.nx) * P.nx;
   T.den = T.cy + size_t(P.ny) * P.ny;
-  T.fa1 = T.den + size_t(P.nx) * P.ny;
-  T.fb2 = T.fa1 + frag_size(mt, P.ny);
-  T.fa3 = T.fb2 + frag_size(nt, P.nx);
-  T.fb4 = T.fa3 + frag_size(mt, P.ny);
+  const double* f = T.den + size_t(P.nx) * P.ny;
+  for (int g = 0; g < 4; ++g)
+    for (int e = 0; e < 2; ++e) {
+      T.f[g][e] = f;
+      f += pma_frag(P, g);
+    }
   return T;
 }
 
@@ -1062,12 +1210,28 @@ std::vector<double> drop_pma_tables(const DropParams& P) {
           f[(size_t(nt) * S + s) * 64 + l] = (k < K && n < N) ? B(k, n) : 0.0;
         }
   };
-  const double* cx = T.cx;
-  const double* cy = T.cy;
-  fill_a(W(T.fa1), ny, ny, [&](int m, int k) { return cy[size_t(m) * ny + k]; });
-  fill_b(W(T.fb2), nx, nx, [&](int k, int n) { return cx[size_t(n) * nx + k]; });
-  fill_a(W(T.fa3), ny, ny, [&](int m, int k) { return cy[size_t(k) * ny + m]; });
-  fill_b(W(T.fb4), nx, nx, [&](int k, int n) { return cx[size_t(k) * nx + n]; });
+  // dct_pair's operands, half index h, k < ceil(N/2): forward even / odd rows of C (the middle
+  // column of an odd N halved on the even side -- it multiplies x_mid + x_mid -- and dropped on
+  // the odd side), inverse C^T by even / odd frequency
+  for (int g = 0; g < 4; ++g) {
+    const int N = g % 2 ? nx : ny, hs = (N + 1) / 2;
+    const double* C = g % 2 ? T.cx : T.cy;
+    auto c = [&](int k, int m) { return C[size_t(k) * N + m]; };
+    auto ent = [&](int odd, int h, int k) -> double {
+      if (g < 2) {
+        if (odd) return (2 * h + 1 < N && 2 * k + 1 != N) ? c(2 * h + 1, k) : 0.0;
+        return 2 * k + 1 == N ? c(2 * h, k) / 2 : c(2 * h, k);
+      }
+      const int fk = 2 * k + odd;
+      return fk < N ? c(fk, h) : 0.0;
+    };
+    for (int e = 0; e < 2; ++e) {
+      if (g % 2 == 0)
+        fill_a(W(T.f[g][e]), hs, hs, [&](int m, int k) { return ent(e, m, k); });
+      else
+        fill_b(W(T.f[g][e]), hs, hs, [&](int k, int n) { return ent(e, n, k); });
+    }
+  }
   return out;
 }
 
@@ -1090,8 +1254,7 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
         hipFuncAttributeMaxDynamicSharedMemorySize, int(kPmaLdsMax));
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(drop_pma_lds_kernel, dim3(1), dim3(DB), lds, s, P, make_coefs(P), M, S, q,
-                       uval, uxx0, uyy0, T.fa1, T.fb2, T.fa3, T.fb4, T.den, dtm, loops, monitor,
-                       tprof);
+                       uval, uxx0, uyy0, T, dtm, loops, monitor, tprof);
   } else {
     hipLaunchKernelGGL(drop_pma_kernel, dim3(1), dim3(DB), 0, s, P, make_coefs(P), M, S, q, uval,
                        uxx0, uyy0, T, dtm, loops, monitor);
@@ -1099,13 +1262,14 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && tprof && !force_global) {
     // debug: per-stage wall-clock (100 MHz) of this launch, to stderr
-    unsigned long long h[5];
+    unsigned long long h[6];
     if (hipMemcpyAsync(h, tprof, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess &&
         hipStreamSynchronize(s) == hipSuccess)
       std::fprintf(stderr,
-                   "pma us/loop: mesh %.2f uders+lap %.2f smooth %.2f rhs %.2f dct %.2f\n",
+                   "pma us/loop: mesh %.2f uders %.2f lap %.2f smooth+integral %.2f rhs %.2f "
+                   "dct %.2f\n",
                    h[0] / 100.0 / loops, h[1] / 100.0 / loops, h[2] / 100.0 / loops,
-                   h[3] / 100.0 / loops, h[4] / 100.0 / loops);
+                   h[3] / 100.0 / loops, h[4] / 100.0 / loops, h[5] / 100.0 / loops);
   }
   return e;
 }
