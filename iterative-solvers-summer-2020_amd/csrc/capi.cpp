@@ -676,6 +676,7 @@ int nk_drop_params_default(nk_drop_params* p) {
 
 int nk_drop_create(nk_drop** out, const nk_drop_params* p, const nk_opts* opts, void* stream) {
   if (!out || !p || p->nx < 7 || p->ny < 7) return NK_EINVAL;
+  if (p->n_exp < 0 || p->m_exp < 0) return NK_EINVAL;  // (integer powers by multiplication)
   DropParams P{};
   P.nx = p->nx;
   P.ny = p->ny;

@@ -167,10 +167,20 @@ __device__ __forceinline__ double lap_axis(const double* v, int sv, const double
   return 0.0;  // the boundary line itself stays zero before the cross term (:615)
 }
 
+// x^n for the small integer exponents of the models (n >= 0) by repeated multiplication.  The
+// reference's NumPy `**` calls libm pow (correctly rounded); this differs from it by a few ulp,
+// where the device pow (an extended-precision log / exp, ~100 instructions) took ~5 us of
+// single-workgroup time per call site and launch.
+__device__ __forceinline__ double ipow(double x, int n) {
+  double r = 1.0;
+  for (int k = 0; k < n; ++k) r *= x;
+  return r;
+}
+
 __device__ __forceinline__ double PI(const DropParams& P, double h) {
   // disjoining pressure (:462-467)
   const double r = P.epsilon / h;
-  return (P.n_exp - 1) * (P.m_exp - 1) * (pow(r, double(P.m_exp)) - pow(r, double(P.n_exp))) /
+  return (P.n_exp - 1) * (P.m_exp - 1) * (ipow(r, P.m_exp) - ipow(r, P.n_exp)) /
          (2 * P.epsilon * (P.n_exp - P.m_exp));
 }
 
@@ -450,7 +460,10 @@ __device__ void lap_pressure_stage(const DropParams& P, const Coefs& C, const Dr
 // compute_P_spatial_ders (:683-694) and the pde_rhs fluxes A, B (:452-457)
 __device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMesh& M, CPlane pr,
                               CPlane u, Plane A, Plane B) {
+  // (point-wise: in column strips this stage and the flux divergence spill registers in the
+  // residual kernel, 44 -> 56 us per launch)
   const int nx = P.nx, ny = P.ny;
+  const double slope = P.Bo * sin(P.alpha2) / P.epsilon2;  // (uniform: once per launch)
   for_points(nx, ny, [&](const int p, const int i, const int j, auto kin) {
     constexpr bool kIn = decltype(kin)::value;
     double pd = dx1<kIn>(C, pr, i, j, nx), pe = dy1<kIn>(C, pr, i, j, ny);
@@ -458,8 +471,8 @@ __device__ void flux_AB_stage(const DropParams& P, const Coefs& C, const DropMes
     if (i == 0 || i == ny - 1) pe = 0.0;
     const double pdx = (M.d2eta[p] * pd - M.dksideta[p] * pe) / M.J[p];
     const double pdy = (-M.dksideta[p] * pd + M.d2ksi[p] * pe) / M.J[p];
-    const double h3 = pow(u(i, j), 3.0);
-    A(i, j) = (pdx - P.Bo * sin(P.alpha2) / P.epsilon2) * h3 / 3;
+    const double h3 = ipow(u(i, j), 3);
+    A(i, j) = (pdx - slope) * h3 / 3;
     B(i, j) = pdy * h3 / 3;
   });
 }
@@ -656,12 +669,12 @@ __global__ void __launch_bounds__(DB) mems_resid_kernel(DropParams P, Coefs Ck, 
             [&](const int p, const int i, const int j, const double vxx, const double vyy) {
               const double w = S.w[p];
               const double g = 1 + w;
-              double r = -Mp.lambd / (g * g) + Mp.lam_eps / pow(g, double(Mp.m));
+              double r = -Mp.lambd / (g * g) + Mp.lam_eps / ipow(g, Mp.m);
               r = r - Mp.beta2 * (vxx + vyy);
               if (i == 0 || j == 0 || i == ny - 1 || j == nx - 1) r = 0.0;  // (:157)
               if (mode == 2) {
                 out[p] = r;
-                red[0] = nmax(red[0], -pow(g, 3.0));
+                red[0] = nmax(red[0], -ipow(g, 3));
                 return;
               }
               const double R = (w - uval[p]) / Mp.k - (r + cn[p]) / 2;  // (:159)
@@ -775,7 +788,7 @@ __global__ void __launch_bounds__(DB) drop_pma_kernel(DropParams P, Coefs Ck, Dr
   double* uyy = S.B;
   for (int it = 0; it < loops; ++it) {
     if (monitor == kMonGap) {
-      FOR_POINTS(NN) { S.ud[p_] = 1 / pow(1 + uval[p_], 6.0); });  // (PMA2_nk.py:357)
+      FOR_POINTS(NN) { S.ud[p_] = 1 / ipow(1 + uval[p_], 6); });  // (PMA2_nk.py:357)
       if (it > 0) {
         mesh_stage(P, C, q, nx, M);
       }
@@ -964,7 +977,7 @@ __global__ void __launch_bounds__(DB) drop_pma_lds_kernel(
         mesh_stage(P, C, L0, ld, M);
         __syncthreads();
       }
-      FOR_POINTS(NN) { L0[i_ * ld + j_] = 1 / pow(1 + uval[p_], 6.0); });  // (PMA2_nk.py:357)
+      FOR_POINTS(NN) { L0[i_ * ld + j_] = 1 / ipow(1 + uval[p_], 6); });  // (PMA2_nk.py:357)
     } else if (it > 0) {
       // compute_Q_spatial_ders + J (:595-596) from q in L0; A11 -> L1, A22 -> L2
       mesh_stage(P, C, L0, ld, M, L1, L2, it == loops - 1);
