@@ -29,11 +29,23 @@ P.d = P.endr - P.endl
 P.dksi = P.d / (P.N - 1)
 P.dksi2 = P.dksi * P.dksi
 
-D1 = _d1_matrix(P.N, P.dksi)    # A.2 (:195-201)
-D2 = _d2_matrix(P.N, P.dksi2)   # A.1 (:184-193)
-_I = np.arange(P.NN).reshape(P.N, P.N)
-IB = SimpleNamespace(Left=_I[:, 0], Right=_I[:, -1], Bottom=_I[0, :], Top=_I[-1, :])
-IB.Boundary = np.unique(np.concatenate([IB.Left, IB.Right, IB.Bottom, IB.Top]))  # make_Ibdy (:164-178)
+
+def configure(n):
+    """The grid-dependent globals for an n x n grid (the reference's N = 51; other sizes exercise
+    the GPU path's even / odd DCT split on both parities of N)."""
+    global D1, D2, _I, IB
+    P.N = n
+    P.NN = n * n
+    P.dksi = P.d / (n - 1)
+    P.dksi2 = P.dksi * P.dksi
+    D1 = _d1_matrix(n, P.dksi)    # A.2 (:195-201)
+    D2 = _d2_matrix(n, P.dksi2)   # A.1 (:184-193)
+    _I = np.arange(P.NN).reshape(n, n)
+    IB = SimpleNamespace(Left=_I[:, 0], Right=_I[:, -1], Bottom=_I[0, :], Top=_I[-1, :])
+    IB.Boundary = np.unique(np.concatenate([IB.Left, IB.Right, IB.Bottom, IB.Top]))  # make_Ibdy (:164-178)
+
+
+configure(P.N)
 
 
 def dksi(v):

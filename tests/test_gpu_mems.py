@@ -62,6 +62,32 @@ def test_steps(mems):
     assert abs(mems.time - float(np.sum(s["dt"]))) <= 1e-15
 
 
+@pytest.mark.parametrize("n", [50, 37])
+def test_steps_other_grids_vs_oracle(n):
+    """PMA2 steps on grids other than the reference's 51 x 51 against the oracle restatement at
+    the same size: an even N takes the PMA solve's even / odd DCT split with no middle entry, an
+    odd one a middle entry on another tile layout.  Tolerances as test_steps."""
+    import nkhip
+    from oracle import pma2_oracle as O
+    O.configure(n)
+    try:
+        unew, qval = O.initial_state()
+        m = nkhip.Mems(n=n)
+        try:
+            m.set_state(unew, qval)
+            for i in range(2):
+                dt = m.step()
+                unew, qval, dto = O.step(unew, qval)
+                U, Q = m.state()
+                assert abs(dt - dto) <= 1e-17, i
+                assert np.abs(U.cpu().numpy() - unew).max() <= 1e-9, i
+                assert _rel(Q, qval) <= 1e-12, i
+        finally:
+            m.close()
+    finally:
+        O.configure(51)
+
+
 def test_run_until(mems):
     dts = mems.run(Tf=3.5e-4)
     assert len(dts) == 4 and mems.time >= 3.5e-4
