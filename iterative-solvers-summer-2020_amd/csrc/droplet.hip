@@ -1103,7 +1103,7 @@ hipError_t drop_resid_launch(const DropParams& P, DropMesh M, DropScratch S, con
                              double omega, const double* prm) {
   if (!shape_ok(P)) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
-  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
+  const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;  // (read per launch: tests flip it)
   if (!force_global && lds <= kPmaLdsMax) {
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&drop_resid_kernel<true>),
@@ -1133,7 +1133,7 @@ hipError_t mems_resid_launch(const DropParams& P, const MemsParams& Mp, DropMesh
                              const double* znorm2, double omega, const double* prm) {
   if (!shape_ok(P) || mode < 0 || mode > 2) return hipErrorInvalidValue;
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
-  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
+  const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;  // (read per launch: tests flip it)
   if (!force_global && lds <= kPmaLdsMax) {
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&mems_resid_kernel<true>),
@@ -1260,7 +1260,7 @@ hipError_t drop_pma_launch(const DropParams& P, DropMesh M, DropScratch S, doubl
     return t;
   }();
   const size_t lds = 3 * size_t(P.ny) * (P.nx | 1) * sizeof(double);
-  static const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;
+  const bool force_global = env_flag("NKHIP_DROP_GLOBAL") != 0;  // (read per launch: tests flip it)
   if (!force_global && lds <= kPmaLdsMax) {
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&drop_pma_lds_kernel),

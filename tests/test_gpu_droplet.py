@@ -114,3 +114,15 @@ def test_initialise_coalescing_reproduces_reference_init_file(tmp_path):
         assert np.array_equal(U2, U.cpu().numpy()) and np.array_equal(Q2, Q.cpu().numpy())
     finally:
         d.close()
+
+
+
+def test_global_memory_fallback(drop, monkeypatch):
+    """The droplet kernels' fallback for grids whose planes do not fit LDS (every field in global
+    scratch, the PMA loop's plain dense DCT; NKHIP_DROP_GLOBAL=1 forces it, read per launch)
+    against the same reference fixtures as the LDS path: the residual and Q after 5 PMA loops."""
+    monkeypatch.setenv("NKHIP_DROP_GLOBAL", "1")
+    f = load_golden("droplet_fields")
+    assert _rel(drop.residual(f["u1"], float(f["dt"])), f["R1"]) <= 1e-11
+    drop.pma(3e-9, 5)
+    assert _rel(drop.field("Q_val"), load_golden("droplet_pma")["Q_5"]) <= 1e-10
