@@ -8,6 +8,12 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+# torch before the library: both need libamdhip64.so.7, and whichever loads first serves the
+# process.  With libnkhip first, ROCm's runtime is bound and torch runs on it -- a fresh process
+# that imported nkhip before torch then failed nk_drop_create with out-of-device-memory
+# (scripts/dbg/drop_create_probe.py); torch first, both run on torch's.
+import torch  # noqa: E402,F401
+
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnkhip.so")
 # NKHIP_LIB: an alternative build of the same C-ABI (kernel tuning builds, `make tune`)
 LIB_PATH = os.environ.get("NKHIP_LIB") or LIB_PATH
