@@ -1637,6 +1637,9 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& oc
                        bool has_mb, int cw, ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
   if (occ.ncu == 0 || occ_mb.ncu == 0) return hipErrorUnknown;
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
+  // the shortest band (NKHIP_ARN_MIN_RY, default 8 rows): short slabs trade resident waves for
+  // fewer band prologues
+  static const int min_ry = env_int("NKHIP_ARN_MIN_RY", 8) > 0 ? env_int("NKHIP_ARN_MIN_RY", 8) : 8;
   const int64_t strips = (A.nx + cw - 1) / cw;
   const int64_t rb = A.r_begin, re = (A.r_end >= 0) ? A.r_end : A.ny;
   if (rb < 0 || re > A.ny || re <= rb) return hipErrorInvalidValue;
@@ -1655,7 +1658,7 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& oc
     p.nbands = target / p.wpr;
     const int64_t cap_bands = A.partial_cap / ((2 * int64_t(NV) + 3) * p.wpr);
     if (p.nbands > cap_bands) p.nbands = cap_bands;
-    if (p.nbands > rows / 8) p.nbands = rows / 8;
+    if (p.nbands > rows / min_ry) p.nbands = rows / min_ry;
     if (p.nbands < 1) p.nbands = 1;
     if (mbox && p.nbands >= 8) p.nbands -= p.nbands % 8;
     p.RY = (rows + p.nbands - 1) / p.nbands;
