@@ -45,3 +45,19 @@ def test_steps():
         assert _rel(q, s["Q_val"][i]) <= 1e-13
         assert abs(dt - s["dt"][i]) <= 1e-18
         assert st.nit == s["nit"][i] and st.nfev == s["nfev"][i]
+
+
+def test_configure_other_grid_and_back():
+    """configure(n) rebuilds every grid-dependent global (the GPU test of other grid sizes uses
+    it); configure(51) restores the reference's grid exactly, so the fixture tests still hold."""
+    D1, D2 = O.D1.copy(), O.D2.copy()
+    try:
+        O.configure(37)
+        assert O.P.N == 37 and O.P.NN == 37 * 37 and O.D1.shape == (37, 37)
+        assert O.IB.Boundary.size == 4 * 37 - 4
+        u, q = O.initial_state()
+        assert u.shape == q.shape == (37 * 37,)
+        assert np.isfinite(O.solve_pma(O.u_ders(u, O.q_ders(q)), O.q_ders(q))).all()
+    finally:
+        O.configure(51)
+    assert np.array_equal(O.D1, D1) and np.array_equal(O.D2, D2) and O.P.NN == 51 * 51
