@@ -57,8 +57,8 @@ def parse():
     ap.add_argument("--probes", choices=["on", "off"], default="on",
                     help="the isolated-JVP and copy-bandwidth probes after the timed region")
     ap.add_argument("--slab-ab", type=int, default=2,
-                    help="N > 1: time steps of each slab-exchange variant after the timed region "
-                         "(slab_exchange_ab; 0: off)")
+                    help="N > 1: time steps of each slab-exchange variant after the warmup; the "
+                         "fastest is the one the timed region runs (slab_exchange_ab; 0: off)")
     return ap.parse_args()
 
 
@@ -426,6 +426,53 @@ def config5_one_gpu(n=16384, warmup=1, steps=1):
             "newton_its_per_step": nit / steps, "arnoldi_steps_per_step": narn / steps}
 
 
+def config4_trajectory(n=4096, steps=100):
+    """Config 4 over its stated length (BASELINE.json: "100 implicit time steps"): the
+    reference's time loop (sh_scipy_nk.py:53-61) from U0 = default_rng(2020).standard_normal(N^2)
+    at N = n (d = 0.625 N, k = 0.2, r = 0.01, g = 1, scipy-default tolerances, FD JVP), all `steps`
+    steps timed from the first (no warmup step skipped: the headline's window starts later on the
+    same trajectory), on a stepper of its own.  steps/s over the whole trajectory, Newton /
+    Arnoldi counts, and the last step's oracle residual (sh_scipy_nk.py:47-49) on the host."""
+    import numpy as np
+    import torch
+
+    import nkhip
+    from oracle import sh_oracle
+    h, k, r, g = 0.625, 0.2, 0.01, 1.0
+    a = torch.as_tensor(np.random.default_rng(2020).standard_normal((n, n)), device="cuda")
+    b = torch.empty_like(a)
+    m = nkhip.SwiftHohenberg(N=n, d=h * n, k=k, r=r, g=g)
+    tot = {"nit": 0, "njvp": 0, "nfev": 0}
+    nit_first = nit_last = None
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        m.step(a, out=b)
+        st = m.last_stats
+        for key in tot:
+            tot[key] += st[key]
+        nit_first = st["nit"] if s == 0 else nit_first
+        nit_last = st["nit"]
+        a, b = b, a
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m.close()
+    u1, u0 = a.cpu().numpy().reshape(-1), b.cpu().numpy().reshape(-1)
+    del a, b
+    torch.cuda.empty_cache()
+    F = sh_oracle.residual(u1, u0, n, n, h, r, k, g)
+    return {"workload": f"swift_hohenberg_cn_newton_krylov_{n}x{n}_{steps}_steps",
+            "steps": steps, "gpu_steps_per_s": round(steps / dt, 4), "seconds": round(dt, 3),
+            "newton_its_per_step": tot["nit"] / steps,
+            "newton_its_first_last": [nit_first, nit_last],
+            "arnoldi_steps_per_step": tot["njvp"] / steps,
+            "ms_per_arnoldi_step": round(1e3 * dt / max(tot["njvp"], 1), 4),
+            "final_step_residual": float(np.abs(F).max()),
+            "f_tol": float(np.finfo(float).eps ** (1 / 3)), "state_max_abs": float(np.abs(u1).max()),
+            "what": "steps 1..%d of the reference's time loop from U0, every step timed; "
+                    "final_step_residual = oracle residual of the last step on the host" % steps}
+
+
 def config_droplet_init():
     """initialise_coalescing_droplets(1000, [[0,0,1,1],[3,0,1,1]], 5e-9, 20) on
     the GPU (20 000 PMA loops); checked against the reference's initdrop_coal_* file."""
@@ -522,6 +569,24 @@ def copy_bandwidth(n, reps=20, scale=4):
                     "HIP events around the back-to-back launches, after the timed region"}
 
 
+_PUSH_FALLBACK = {"set": False}  # peer_or_rccl set NKHIP_SLAB_PUSH=0 itself
+
+
+def effective_slab_path(slots, one_device):
+    """The slab path the solver takes on a peer-memory group under the current environment (the
+    switches the library reads per call): in_kernel (NKHIP_SLAB_XK, sh_problem.cpp push_mode),
+    edge_halo (no halo slots, or NKHIP_SLAB_PUSH=0), pushed_tail (NKHIP_ARN_TAIL, one rank per
+    GPU only, lgmres.cpp), else pushed."""
+    xk = os.environ.get("NKHIP_SLAB_XK", "")
+    if xk[:1] == "1" or (xk[:1] == "2" and not one_device):
+        return "in_kernel"
+    if not slots or os.environ.get("NKHIP_SLAB_PUSH", "1")[:1] == "0":
+        return "edge_halo"
+    if os.environ.get("NKHIP_ARN_TAIL", "")[:1] in ("1", "2") and not one_device:
+        return "pushed_tail"
+    return "pushed"
+
+
 def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cpu", allow_rccl=True):
     """The peer-memory communicator, verified before it is used, at the full row width, with
     bounded device waits.  Two collectives, each agreed on over the gloo side channel:
@@ -551,16 +616,21 @@ def peer_or_rccl(nkhip, dist, torch, max_nx, coll_dev="cpu", allow_rccl=True):
         check = {"selftest": "ok"}
         if push is None:
             check["pushed_rows_selftest"] = "n/a (no halo slots)"
-            check["slab_path"] = "edge_halo"
         elif push_ok == 1:
             check["pushed_rows_selftest"] = "ok"
-            check["slab_path"] = "pushed"
+            # a fallback an earlier group of this run set is not this group's (config 5 builds a
+            # second group): only the switch this function set itself is taken back
+            if _PUSH_FALLBACK["set"]:
+                os.environ.pop("NKHIP_SLAB_PUSH", None)
+                _PUSH_FALLBACK["set"] = False
         else:
             print("pushed-halo-rows self-test failed on some rank: every rank takes the edge + "
                   "halo exchange path (NKHIP_SLAB_PUSH=0)", file=sys.stderr)
             os.environ["NKHIP_SLAB_PUSH"] = "0"
+            _PUSH_FALLBACK["set"] = True
             check["pushed_rows_selftest"] = "failed on some rank"
-            check["slab_path"] = "edge_halo"
+        # the path the solver takes: from the effective switches, not from the test alone
+        check["slab_path"] = effective_slab_path(push is not None, not allow_rccl)
         return comm, check
     print("peer-memory communicator failed its self-test on some rank"
           + (": using RCCL" if allow_rccl else ""), file=sys.stderr)
@@ -598,6 +668,17 @@ def slab_residual_max(nkhip, dist, torch, u1, u0, n, rank, world, h, r, k, g):
     return float(worst.item())
 
 
+def slab_of_seeded_grid(seed, n, row0, ny, chunk=256):
+    """Rows [row0, row0 + ny) of default_rng(seed).standard_normal((n, n)) without materialising
+    the rows before them: the generator's draws are sequential, so drawing and discarding the
+    leading rows in chunks of `chunk` rows gives the same numbers in bounded host memory."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    for r0 in range(0, row0, chunk):
+        rng.standard_normal((min(chunk, row0 - r0), n))
+    return rng.standard_normal((ny, n))
+
+
 def config5_slabs(nkhip, dist, torch, comm, check, n5, rank, world, one_device, steps=1,
                   warmup=1):
     """Config 5 on the N ranks of this job: the 16384^2 grid (d = 0.625 N, k, r, g and seed as the
@@ -613,9 +694,8 @@ def config5_slabs(nkhip, dist, torch, comm, check, n5, rank, world, one_device, 
         comm, check = peer_or_rccl(nkhip, dist, torch, n5, "cpu", allow_rccl=not one_device)
     h, k, r, g = 0.625, 0.2, 0.01, 1.0
     row0, ny = nkhip.slab_rows(n5, rank, world)
-    # the first row0 + ny rows of default_rng(2020).standard_normal((n5, n5)): the same numbers
-    U = np.random.default_rng(2020).standard_normal((row0 + ny, n5))[row0:]
-    a = torch.as_tensor(np.ascontiguousarray(U), device="cuda")
+    U = slab_of_seeded_grid(2020, n5, row0, ny)
+    a = torch.as_tensor(U, device="cuda")
     del U
     b = torch.empty_like(a)
     dist.barrier()
@@ -742,7 +822,7 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pus
     keys = ("NKHIP_SLAB_PUSH", "NKHIP_SLAB_XK", "NKHIP_ARN_TAIL", "NKHIP_ARN_TAIL_TIMEOUT_S")
     old = {k_: os.environ.get(k_) for k_ in keys}
     acc = {n_: [0.0, 0] for n_ in names}
-    failed = None
+    failed = failed_name = None
     try:
         for i in range(len(names) * rounds):
             name = names[i % len(names)]
@@ -762,6 +842,7 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pus
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             if float(t[1].item()) > 0:
                 failed = failed or f"{name}: failed on another rank"
+                failed_name = name
                 break
             acc[name][0] += float(t[0].item())
             acc[name][1] += model.last_stats["njvp"]
@@ -777,10 +858,36 @@ def slab_exchange_ab(model, a, b, rounds, one_device, dist, coll_dev, torch, pus
         rec["skipped"] = "pushed, pushed_tail (the pushed-halo-rows self-test did not pass)"
     if failed:
         rec["failed"] = failed
+        rec["failed_variant"] = failed_name
     rec.update({"steps_each": rounds, "arnoldi_steps": {k_: v[1] for k_, v in acc.items()},
                 "what": "rotating time steps after the timed region; max over ranks of each "
                         "step's wall time / its Arnoldi steps"})
     return rec, a, b
+
+
+def select_slab_path(rec, one_device, dist, torch):
+    """The fastest slab path of a slab_exchange_ab record (ms per Arnoldi step, max over ranks;
+    variants that failed or ran no step are out), rank 0's choice on every rank; its switches are
+    set in this process's environment for everything after (the library reads them per call).
+    With ranks sharing one GPU the tail is not used (lgmres.cpp), so pushed_tail there is the
+    pushed path."""
+    names = ("pushed", "edge_halo", "in_kernel", "pushed_tail")
+    ok = [n_ for n_ in names if rec.get("arnoldi_steps", {}).get(n_, 0) > 0
+          and n_ != rec.get("failed_variant")]
+    best = min(ok, key=lambda n_: rec[f"{n_}_ms_per_arnoldi"]) if ok else None
+    t = torch.tensor([names.index(best) if best else -1], dtype=torch.int32)
+    dist.broadcast(t, 0)
+    best = names[int(t.item())] if int(t.item()) >= 0 else None
+    env = {"pushed": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
+           "edge_halo": {"NKHIP_SLAB_PUSH": "0", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "0"},
+           "in_kernel": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "1" if one_device else "2",
+                         "NKHIP_ARN_TAIL": "0"},
+           "pushed_tail": {"NKHIP_SLAB_PUSH": "1", "NKHIP_SLAB_XK": "0", "NKHIP_ARN_TAIL": "1",
+                           "NKHIP_ARN_TAIL_TIMEOUT_S": "3"}}
+    if best is None:  # nothing ran: the default switches
+        return effective_slab_path(True, one_device)
+    os.environ.update(env[best])
+    return effective_slab_path(True, one_device)
 
 
 def main():
@@ -850,6 +957,38 @@ def main():
     for _ in range(args.warmup):
         model.step(a, out=b)
         a, b = b, a
+    # N > 1: the slab path the timed region runs is the one that wins on THIS node -- the slab
+    # A/B runs here, after the warmup, and every rank takes its fastest variant (the times are
+    # maxima over ranks, so every rank computes the same winner; rank 0's is broadcast anyway).
+    # The state is restored afterwards, so the timed window starts where it would without it.
+    slab_ab, slab_path = None, ("edge_halo (RCCL)" if world > 1 else None)
+    if world > 1 and comm_check is not None:
+        slab_path = comm_check.get("slab_path")
+        if args.slab_ab > 0:
+            a_keep = a.clone()
+            pushed_ok = comm_check.get("slab_path") == "pushed"
+            slab_ab, a, b = slab_exchange_ab(model, a, b, args.slab_ab, one_device, dist,
+                                             coll_dev, torch, pushed_ok=pushed_ok)
+            slab_path = select_slab_path(slab_ab, one_device, dist, torch)
+            a.copy_(a_keep)
+            del a_keep
+            if slab_ab.get("failed"):
+                # a variant that failed may have left the group's error word set: a fresh group
+                # and stepper for the timed region (the winner's switches are already in place)
+                model.close()
+                comm.abort()
+                comm.close()
+                dist.barrier()
+                comm, comm_check = peer_or_rccl(nkhip, dist, torch, args.n, coll_dev,
+                                                allow_rccl=not one_device)
+                slab_path = comm_check.get("slab_path")
+                dist.barrier()
+                model = nkhip.SwiftHohenberg(N=n, d=h * n, k=k, r=r, g=g, jvp=args.jvp,
+                                             profile=profile, comm=comm, ny_local=ny,
+                                             stream=stream)
+            slab_ab.update({"selected": slab_path,
+                            "when": "after the warmup, before the timed region (the warmup's "
+                                    "final state is restored for the timed steps)"})
     want_cpu = world == 1 and args.cpu_baseline == "auto"
     u_start = a.cpu().numpy().reshape(-1) if want_cpu else None  # outside the timed region
     model.reset_profile()
@@ -889,11 +1028,6 @@ def main():
         full_a, full_b = gather(a), gather(b)
     else:
         full_a, full_b = a.cpu().numpy(), b.cpu().numpy()
-    slab_ab = None
-    if world > 1 and args.slab_ab > 0:
-        slab_ab, a, b = slab_exchange_ab(model, a, b, args.slab_ab, one_device, dist, coll_dev,
-                                         torch, pushed_ok=(comm_check or {}).get("slab_path")
-                                         == "pushed")
     # config 5 on this job's ranks (N > 1): the point of the 16384^2 curve; at N = 1 it runs
     # below, in other_configs.config5_1gpu
     c5 = None
@@ -940,7 +1074,11 @@ def main():
                     "traffic": traffic, "launches": v["launches"], "timed_launches": v["timed"],
                     "avg_us": round(1e3 * v["ms"] / v["timed"], 2),
                     "alg_bytes_per_launch": alg,
-                    "traffic_source": traffic_db.get("source") if traffic else None}
+                    "traffic_source": (traffic_db.get("source") if live else
+                                       f"N=1 profile ratios, tag {traffic_db.get('tag')} "
+                                       f"(profiles/latest_traffic.json: "
+                                       f"{traffic_db.get('source')}); not measured in this run")
+                    if traffic else None}
 
         from oracle import sh_oracle
         F_last = sh_oracle.residual(full_a.reshape(-1), full_b.reshape(-1), n, n, h, r, k, g)
@@ -969,6 +1107,7 @@ def main():
                        "h": h, "k": k, "r": r, "g": g, "jvp": args.jvp,
                        "f_tol": "scipy default eps^(1/3) (max-norm)", "inner_m": 30,
                        "outer_k": 10, "parallelism": f"row-slab x{world}",
+                       "slab_path": slab_path,
                        "comm": (type(comm).__name__ if comm is not None else "none")},
             "comm_check": comm_check,
             "newton_its_per_s": round(tot["nit"] / elapsed, 3),
@@ -1041,6 +1180,7 @@ def main():
             out["other_configs"] = {"config5": c5}
         if world == 1 and args.extra == "on":
             out["other_configs"] = {"config2": config2_lap5(rocprof=args.pmc == "auto"),
+                                    "config4_100": config4_trajectory(n),
                                     "config3": config3_droplet(),
                                     "config5_1gpu": config5_one_gpu(),
                                     "pma2": config_pma2(), "sh_linearised": config_shlin(),
@@ -1048,8 +1188,11 @@ def main():
         print(json.dumps(out), flush=True)
         # a wrong answer fails the run (sh_scipy_nk.py:47-49: the step is a root to f_tol in the
         # max norm; the slack covers the oracle's own rounding, ~1e-14 at these magnitudes)
+        c4 = out.get("other_configs", {}).get("config4_100") or {}
         for what, v, tol in (("headline", final_check["max_abs_residual"], final_check["f_tol"]),
                              ("config5", (c5 or {}).get("final_step_residual", 0.0),
+                              final_check["f_tol"]),
+                             ("config4_100", c4.get("final_step_residual", 0.0),
                               final_check["f_tol"])):
             if not v <= tol + 1e-12:
                 print(f"bench: {what} final-step residual {v:.3e} exceeds f_tol {tol:.3e}",

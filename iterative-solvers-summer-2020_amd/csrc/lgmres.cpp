@@ -179,9 +179,10 @@ int NewtonKrylov::lgmres(double tol, double* dnorm, double* dmax, double** dvec)
     const double* z;
     double zs, zn;
     input(0, &z, &zs, &zn);
-    // the line search's speculative JVP applied J to this same input at this same point
+    // the line search's speculative JVP applied J to this same input at this same point (the
+    // accepted trial's pool vectors are the iterate and its G now)
     const bool have = spec_.valid && n_o > 0 && z == spec_.z && zs == spec_.zs &&
-                      zn == spec_.zn && V_[1] == spec_.w;
+                      zn == spec_.zn && V_[1] == spec_.w && X_ == spec_.x && G0_ == spec_.g;
     spec_.valid = false;
     rc = issue_step(0, z, zs, zn, false, have);
   }
@@ -436,6 +437,9 @@ int NewtonKrylov::device_steps() {
   };
   Rot rot[kMaxVec + 2];
   double cc[kMaxVec] = {};  // the launch arguments the parameter block overrides
+  // the tail's wait bound, read per run of device steps (NKHIP_PEER_TIMEOUT_S may change between
+  // runs: bench legs, tests)
+  const uint64_t wait_ticks = device_wait_ticks();
   // the control of step t on the (all-reduced) multi-dot results in its slot
   // the control of step t on the (all-reduced) multi-dot results in its slot; `copy`: the
   // results also to the host slot (the all-reduce path leaves out its own D2H copy)
@@ -510,7 +514,7 @@ int NewtonKrylov::device_steps() {
       tl.t = t + 1;
       tl.nval = nval;
       tl.peer = !one;
-      static const uint64_t ticks = device_wait_ticks();
+      const uint64_t ticks = wait_ticks;
       tl.wait_ticks = ticks;
       if (have_pa) tl.pa = pa;
       // NKHIP_ARN_TAIL_TIMEOUT_S (read per launch): a shorter bound for the tail's waits -- its

@@ -585,6 +585,8 @@ int NewtonKrylov::line_search(double* s_out, double* fnorm_new, double* fmax, do
         spec_.zs = sp.zs;
         spec_.zn = sp.zn;
         spec_.w = sp.w;
+        spec_.x = Xt_;  // the trial this eval wrote (phi(1.0): Xt_, Gt_)
+        spec_.g = Gt_;
       } else {
         E_.void_last(K_FDJVP, 1);  // a launch that did nothing
       }

@@ -342,12 +342,15 @@ class NewtonKrylov {
   double fx_norm_ = 0.0;
   double rdiff_ = 0.0;
   double f_tol_ = 0.0;
-  // the speculative first JVP of the next LGMRES call (line_search): ran on the device
+  // the speculative first JVP of the next LGMRES call (line_search): ran on the device at the
+  // trial point x with G(x) = g (the pool vectors an accepted s = 1 swaps into X_ / G0_)
   struct {
     bool valid = false;
     const double* z = nullptr;
     double zs = 0.0, zn = 0.0;
     double* w = nullptr;
+    const double* x = nullptr;
+    const double* g = nullptr;
   } spec_;
 };
 

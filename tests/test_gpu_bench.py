@@ -39,6 +39,13 @@ def test_bench_self_launch_four_ranks_one_gpu():
     ab = d["slab_exchange_ab"]
     assert all(ab[f"{k}_ms_per_arnoldi"] > 0
                for k in ("pushed", "edge_halo", "in_kernel", "pushed_tail")), ab
+    # the timed region ran the A/B's winner (ranks sharing a GPU take no tail: pushed_tail there
+    # is the pushed path)
+    assert d["config"]["slab_path"] in ("pushed", "edge_halo", "in_kernel", "pushed_tail")
+    assert ab["selected"] == d["config"]["slab_path"]
+    best = min(("pushed", "edge_halo", "in_kernel", "pushed_tail"),
+               key=lambda k: ab[f"{k}_ms_per_arnoldi"])
+    assert d["config"]["slab_path"] == ("pushed" if best == "pushed_tail" else best), ab
     # the roofline names the dominant streaming kernel (with four ranks time-sharing one GPU the
     # slab edge kernel's waits for the other processes are the largest kernel time: excluded)
     assert d["value"] > 0 and d["roofline"]["kernel"] == "arnoldi_fused"
@@ -71,6 +78,8 @@ def test_bench_push_selftest_fault_falls_back_and_config5_leg():
     assert d["comm_check"]["slab_path"] == "edge_halo"
     assert "pushed_ms_per_arnoldi" not in d["slab_exchange_ab"], d["slab_exchange_ab"]
     assert d["slab_exchange_ab"]["edge_halo_ms_per_arnoldi"] > 0
+    # the winner of the two exchange variants, never a pushed one
+    assert d["config"]["slab_path"] in ("edge_halo", "in_kernel"), d["config"]
     fc = d["final_step_check"]
     assert fc["max_abs_residual"] <= fc["f_tol"], fc
     c5 = d["other_configs"]["config5"]
@@ -78,4 +87,21 @@ def test_bench_push_selftest_fault_falls_back_and_config5_leg():
     assert c5["ms_per_arnoldi_step"] > 0 and c5["newton_its_per_step"] >= 1
     assert c5["final_step_residual"] <= c5["f_tol"], c5
     assert c5["comm"] == "PeerComm"
-    assert c5["comm_check"]["slab_path"] == "edge_halo"  # the injected fault holds for its group
+    # the injected fault holds for its group: the headline's winner, never the pushed path
+    assert c5["comm_check"]["slab_path"] == d["config"]["slab_path"], c5["comm_check"]
+
+
+@pytest.mark.timeout(300)
+def test_config4_trajectory_field():
+    """bench.py's other_configs.config4_100 (BASELINE config 4 over its stated length, 100 implicit
+    time steps of sh_scipy_nk.py:53-61 from default_rng(2020)) at a shrunken grid: every step a
+    root of the reference residual, so the last one's oracle residual is within f_tol."""
+    sys.path.insert(0, ROOT)
+    import bench
+    c4 = bench.config4_trajectory(n=128, steps=100)
+    assert c4["steps"] == 100 and c4["gpu_steps_per_s"] > 0, c4
+    assert c4["workload"] == "swift_hohenberg_cn_newton_krylov_128x128_100_steps"
+    assert c4["newton_its_per_step"] >= 1 and c4["arnoldi_steps_per_step"] >= 1
+    assert all(x >= 1 for x in c4["newton_its_first_last"]), c4
+    assert c4["final_step_residual"] <= c4["f_tol"], c4
+    assert c4["ms_per_arnoldi_step"] > 0

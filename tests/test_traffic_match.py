@@ -70,3 +70,25 @@ def test_more_dispatches_than_logged_launches(tmp_path):
     c = tm.match(fetch, write, None, str(log), "t")["classes"]["krylov_combo"]
     assert c["dispatches_matched"] == 1 and c["profiled"] == 3 and c["logged"] == 1
     assert c["traffic_over_alg"] == pytest.approx((2 * 1024 * 50 + 1024 * 10) / 110592)
+
+
+def test_fallback_traffic_file_is_the_newest_profile():
+    """The N > 1 line takes roofline.traffic from profiles/latest_traffic.json (no live PMC pass
+    there): it must be the newest committed profile's per-dispatch match, and every class in it a
+    class that profiled run of the solver launched (the file lists only logged classes)."""
+    import glob
+    import json
+    import re
+    prof = os.path.join(ROOT, "profiles")
+    tagged = {}
+    for p in glob.glob(os.path.join(prof, "r*_traffic.json")):
+        m = re.match(r"r(\d+)([a-z]*)_traffic\.json$", os.path.basename(p))
+        if m:
+            tagged[(int(m.group(1)), m.group(2))] = p
+    newest = tagged[max(tagged)]
+    latest = json.load(open(os.path.join(prof, "latest_traffic.json")))
+    assert latest == json.load(open(newest)), f"latest_traffic.json is not {newest}"
+    assert latest["classes"], latest
+    for name, c in latest["classes"].items():
+        assert c["logged"] > 0 and c["dispatches_matched"] > 0, (name, c)
+        assert c["traffic_over_alg"] and 0.5 < c["traffic_over_alg"] < 2.0, (name, c)
