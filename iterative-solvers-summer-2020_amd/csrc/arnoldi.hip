@@ -32,6 +32,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "arnctl_dev.h"
 #include "nk_device.h"
@@ -297,6 +298,24 @@ __device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0
 }
 
 // ------------------------------------------------------------------------------------------
+// March direction.  A band of rows [r0, r1) also reads its two band-halo rows on either side
+// (the stencil couples rows r-2 .. r+2): r0-2, r0-1 and r1, r1+1, every update entry of them.
+// Those rows are the neighbouring bands' own rows, and marching every band down, a band reads
+// its upper halo at its start while the band above reads the same rows at its END (and vice
+// versa): a whole launch apart, so both reads come from HBM -- on short slabs 4 extra rows per
+// band are a large share (a 512-row slab: PMC traffic 1.15x of algorithmic for the pair layout's
+// 32-row bands, 1.22-1.39x for the wide layout's 8-16-row bands; profiles/r06a_slab512_kernels.txt).
+// With A.alt the even bands march UP their rows: two adjacent bands then reach their shared
+// boundary at the same moment -- both at their start, or both at their end.  The bands of one XCD
+// are a contiguous run starting at an even band (the blockIdx mapping below), so its boundaries
+// 2b | 2b+1 are start-start ones, and the prologue loads its rows temporally (the interior stays
+// non-temporal): the second read of each shared row then hits the XCD's L2.  (Temporal loads for
+// the end rows as well would need a second copy of the row loop; its register allocation spilled.)
+// The kernels run over a logical row index t (prow(t): physical row), so a band's every
+// computation is the same in either direction: v and w' are bitwise the same (the stencil adds
+// the two rows either side of the centre as a + b == b + a), only the order in which a wave
+// accumulates its rows' dot products changes.  Measured in profiles/r06_short_slab.md.
+// ------------------------------------------------------------------------------------------
 // Slab exchange inside the fused kernel (row slabs over the peer-memory communicator, A.x.me set;
 // peer_dev.h holds the buffer layout).  A slab's stencil needs u on the neighbours' two edge rows,
 // and u of a row needs only the basis, not the stencil: so the blocks of the FIRST band compute u
@@ -311,7 +330,7 @@ __device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0
 // this rank's staging rows (A.yh, row stride A.yh_ld).  A wait that gives up (abort, timeout) sets
 // the communicator's error word; the host sees it at its next synchronisation.
 template <int NV>
-__device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW, int h0,
+__device__ __forceinline__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, int64_t BW, int h0,
                                 double a_tau, bool top, bool bot) {
   const SlabX& X = A.x;
   const int64_t nx = A.nx, ny = A.ny;
@@ -377,7 +396,7 @@ __device__ void slab_x_exchange(const ArnoldiArgs& A, int64_t band, int64_t B0, 
 // no block waits for another rank.  (A halo column shared with the neighbouring block is written
 // by both with the same bits.)
 template <int NV>
-__device__ void slab_push_prologue(const ArnoldiArgs& A, bool first, bool last, int64_t B0,
+__device__ __forceinline__ void slab_push_prologue(const ArnoldiArgs& A, bool first, bool last, int64_t B0,
                                    int64_t BW, int h0, const double* cst, double a_tau) {
   const int64_t nx = A.nx, ld = A.hs_ld;
   double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
@@ -453,12 +472,18 @@ __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int
 // must keep (an SGPR, or a VGPR lane when it spills) instead of re-reading it from the kernel
 // arguments
 typedef int ix_t;
-// ARN_OPQ 2 also pins the stencil coefficients and the x0 pointer (doubles / pointers through an
-// "s" asm constraint): the bounds-checked build of that produced NaN at nv 25-30 on the mailbox
-// instantiation without a single out-of-range index (round 5: ARN_OPQ 1 and 0 are clean), so the
-// default pins the 32-bit grid scalars only
-#ifndef ARN_OPQ  // 2: grid scalars, stencil coefficients and x0 pinned; 1: grid scalars; 0: none
+// ARN_OPQ 1 (default) pins the 32-bit grid scalars; 0: none.  A level 2 that also pinned the
+// stencil coefficients and the x0 pointer through "+s" constraints on doubles / pointers is gone:
+// its bounds-checked build of the round-5 kernel returned w' scaled by one constant (1.5e-9 x the
+// true value) on every row of each band but the first, v exact, at nv 25 -- the loop-invariant FD
+// scale read wrongly after the row loop's first iteration, identically with no mailbox record ever
+// polled (NKHIP_ARN_MBOX=2) and with zero out-of-range indices: a code-generation fault of that
+// instantiation, not a race (round 6, scripts/dbg/opq2_probe.py, opq2_pattern.py)
+#ifndef ARN_OPQ
 #define ARN_OPQ 1
+#endif
+#if ARN_OPQ > 1
+#error "ARN_OPQ 2 (pinned coefficients and x0) is removed: see the note above"
 #endif
 template <bool PIN = true>
 __device__ __forceinline__ int opaque_s(int x) {
@@ -470,14 +495,6 @@ __device__ __forceinline__ int opaque_s(int x) {
 // either way, and 6 % slower with the scalars pinned; round 5, profiles/r05_arnoldi_short_end.md)
 template <int NV>
 constexpr bool kPinScalars = NV <= 33;
-__device__ __forceinline__ double opaque_d(double x) {
-  if constexpr (ARN_OPQ >= 2) asm volatile("" : "+s"(x));
-  return x;
-}
-__device__ __forceinline__ const double* opaque_p(const double* p) {
-  if constexpr (ARN_OPQ >= 2) asm volatile("" : "+s"(p));
-  return p;
-}
 
 // Lane layout ("vector pairs"): a wave owns 64 aligned columns; lane l of half hf (lane = 32 hf + l)
 // holds columns 2l, 2l+1 (one 16-B load) of entry 2k + hf of the row's load list
@@ -530,7 +547,7 @@ __device__ unsigned long long g_tail_diag[8];
 constexpr int kTailR = 8;
 constexpr int kTailC = (2 * kArnMaxNV + 3 + kTailR - 1) / kTailR;  // values per reducer
 template <int BS>
-__device__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArnMaxNV + 1]) {
+__device__ __forceinline__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, double (*G)[kArnMaxNV + 1]) {
   const ArnTail& T = A.tail;
   __shared__ uint32_t ticket;
   __shared__ bool ok;
@@ -723,15 +740,14 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const ix_t r0 = opaque_s<kPinScalars<NV>>(ix_t(A.r_begin) + band * A.RY);
   const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
   const ix_t nrows = r1 - r0;
-  // the stencil coefficients in registers for the whole loop (re-read from the kernel
-  // arguments per row otherwise: a scalar load and an lgkmcnt wait each)
-  SHCoef K = A.k;
-  K.c0 = opaque_d(K.c0);
-  K.c1 = opaque_d(K.c1);
-  K.c2 = opaque_d(K.c2);
-  K.c3 = opaque_d(K.c3);
-  K.g = opaque_d(K.g);
-  K.ik = opaque_d(K.ik);
+  // march direction ("March direction" above): logical row t of the band is physical row
+  // rb + rs t -- r0 + t marching down, r1 - 1 - t marching up (odd bands under A.alt)
+  const bool dn = A.alt <= 0 || (band & 1) == 1;
+  const ix_t rb = opaque_s<kPinScalars<NV>>(dn ? r0 : r1 - 1);
+  const ix_t rs = dn ? 1 : -1;
+  using NTc = std::integral_constant<bool, NT>;
+  using TMc = std::integral_constant<bool, false>;
+  const SHCoef K = A.k;
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.out_w, ny * nx);
@@ -799,7 +815,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   auto eoff = [&](ix_t q) -> uint32_t {
     return eOn ? uint32_t(CI((ebo / 4) * ny * 4 + q * 4 + (ebo & 3), eelem - 1) * 8) : kOOB;
   };
-  const double* x0p = opaque_p(A.x0);  // (kept in registers, as the grid scalars above)
+  const double* x0p = A.x0;
   const double* hxp = (EXT && lane >= 4) ? A.z : x0p;  // lanes 0-3: x0 halo, 4-7: z halo
   // row slab: rows -2, -1, ny, ny+1 are the neighbours' -- their u arrives in A.yh (the x0 entry
   // and the x0 halo lanes read it there in place of x0)
@@ -807,13 +823,18 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const double* yhb = slab ? A.yh : A.x0;
   const ix_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
 
-  auto wrap = [&](ix_t q) -> ix_t {
-    q = (q > r1 + 1) ? r1 + 1 : q;  // past the band halo: re-read its last row
+  // physical row of logical row t (past the band halo: its last row, re-read), -2 .. ny + 1
+  auto prow = [&](ix_t t) -> ix_t {
+    t = (t > nrows + 1) ? nrows + 1 : t;
+    return rb + rs * t;
+  };
+  auto wrap = [&](ix_t t) -> ix_t {  // ... periodic
+    const ix_t q = prow(t);
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
   // a neighbour slab's halo row (u taken from A.yh)
-  auto halo_row = [&](ix_t q) -> bool {
-    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
+  auto halo_row = [&](ix_t t) -> bool {
+    const ix_t qc = prow(t);
     return slab && (qc < 0 || qc >= ny);
   };
 
@@ -832,11 +853,11 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const ix_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;  // the halo pair's columns
   // this lane stopped polling (a neighbour was not there in time; mb_recompute: test switch)
   bool mb_dead = A.mb_recompute;
-  auto mb_need = [&](ix_t q) -> bool { return (needL || needR) && !halo_row(q); };
-  auto poll = [&](ix_t q, u32x4* a, u32x4* b) {  // issue the two record loads of row q
-    const bool on = mb_need(q) && !mb_dead;
-    const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
-    ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
+  auto mb_need = [&](ix_t t) -> bool { return (needL || needR) && !halo_row(t); };
+  auto poll = [&](ix_t t, u32x4* a, u32x4* b) {  // issue the two record loads of row t
+    const bool on = mb_need(t) && !mb_dead;
+    const uint32_t o = mb_off(Lnb, mbT, t + 2, nside, 0);
+    ARN_CHK(!on || (t + 2 >= 0 && t + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
     *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
     *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
   };
@@ -846,8 +867,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     return e < NV ? A.V[e] : (e == NV ? A.w : ((e == EX || !EXT) ? A.x0 : A.z));
   };
   auto cfd = [&](int e) -> double { return e < NV ? arn_c(A, e) : (e == NV ? a_tau : 0.0); };
-  auto recompute = [&](ix_t q) -> dv2 {
-    const ix_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
+  auto recompute = [&](ix_t t) -> dv2 {
+    const ix_t o2 = CI(wrap(t) * nx + fcol, nelem - 1);
     double p0x = 0.0, p0y = 0.0, p1x = 0.0, p1y = 0.0;
 #pragma unroll 1
     for (int k = 0; k < NI; ++k) {
@@ -863,14 +884,14 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     return dv2{p0x + p1x, p0y + p1y};
   };
   // the halo pair of row q (-0.0 where the lane needs none: adding it changes nothing)
-  auto mb_halo = [&](ix_t q, u32x4 a, u32x4 b) -> dv2 {
-    const bool need = mb_need(q);
+  auto mb_halo = [&](ix_t t, u32x4 a, u32x4 b) -> dv2 {
+    const bool need = mb_need(t);
     bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
     if (need) MB_STAT(0, 1);
     dv2 h{mb_val(a), mb_val(b)};
     if (!ok) {  // the neighbour is behind (or was not there): poll, then recompute
       MB_STAT(1, 1);
-      const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+      const uint32_t o = mb_off(Lnb, mbT, t + 2, nside, 0);
       int n = 0;
       for (; n < kMBSpin && !mb_dead && !ok; ++n) {
         __builtin_amdgcn_s_sleep(2);
@@ -884,7 +905,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       } else {
         MB_STAT(3, 1);
         mb_dead = true;
-        h = recompute(q);
+        h = recompute(t);
       }
     }
     return need ? h : dv2{-0.0, -0.0};
@@ -896,18 +917,22 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     double hx;
     bool own;  // row of this slab (false: a neighbour's halo row, u taken from A.yh)
   };
-  auto load = [&](Slot& s, ix_t q) {
-    const ix_t qq = wrap(q);
+  // pol: the streamed loads' cache policy -- NTc (non-temporal where NT is set) in the row loop,
+  // TMc (temporal) in the prologue, whose rows the neighbouring band reads as well ("March
+  // direction").  A compile-time choice: a runtime select between the two load forms is merged
+  // into one plain load (the non-temporal hint dropped)
+  auto load = [&](Slot& s, ix_t t, auto pol) {
+    const ix_t qq = wrap(t);
     const ix_t o = CI(qq * nx + col, nelem - 1);
-    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;  // the row wrap() reads (-2 <= qc <= ny + 1)
-    const bool hrow = halo_row(q);
+    const ix_t qc = prow(t);  // the row wrap() reads (-2 <= qc <= ny + 1)
+    const bool hrow = halo_row(t);
     const ix_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;  // row of A.yh, 0..3
     const ix_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const double* a = ep[k] + o;
       if (k == EX / 2) a = (hrow && hf == (EX & 1)) ? yhb + yo : a;
-      s.e[k] = gld2<NT>(a);
+      s.e[k] = gld2<decltype(pol)::value>(a);
     }
     const ix_t ho = CI(qq * nx + hcol, nelem);
     // block halo: from the entry's edge array (four rows per line) or from the vector itself;
@@ -931,9 +956,9 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     const bool mine = hf == (e & 1);
     return dv2{mine ? x.x : px, mine ? x.y : py};
   };
-  // the basis entries and x0 of row q wait in LDS slot (q - r0) & 1 until row q's dot products
-  auto stash = [&](const Slot& s, const dv2& g, ix_t q) {
-    dv2 (*d)[64] = lg[(q - r0) & 1];
+  // the basis entries and x0 of row t wait in LDS slot t & 1 until row t's dot products
+  auto stash = [&](const Slot& s, const dv2& g, ix_t t) {
+    dv2 (*d)[64] = lg[t & 1];
 #pragma unroll
     for (int k = 0; k < NB; ++k) d[k][lane] = s.e[k];
     d[NB][lane] = g;
@@ -944,7 +969,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
 #pragma unroll
   for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
   dv2 gq{0.0, 0.0};  // x0 of the last pushed row (both halves)
-  auto push = [&](const Slot& s, ix_t q) {
+  auto push = [&](const Slot& s, ix_t t) {
+    const ix_t q = prow(t);  // (its physical row; stored only when it is one of the band's)
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {  // explicit FMAs: the mailbox's recompute() repeats them
@@ -965,13 +991,13 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
     // block halo: this wave's share of c_i V_i on the four halo columns (sum over the 16 lanes
     // of each column), exchanged with u on the edge columns of every wave through LDS
-    const int slot = int(q & 1);
+    const int slot = int(t & 1);
     // mailbox: publish u on this block's first / last column pair
     {
       if constexpr (mb) {
         const bool pq = prod && s.own;
-        const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
-        ARN_CHK(!pq || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
+        const uint32_t po = mb_off(L, mbT, t + 2, pside, 0);
+        ARN_CHK(!pq || (t + 2 >= 0 && t + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
                                                kMBCoh);
@@ -1034,7 +1060,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     vw[4] = v;
     // the h2 = u[c-2] + u[c+2] of row q is needed only when q is the window centre: keep the
     // four outer neighbours of the row two steps back
-    const bool st = own && hf == 0 && q >= r0 && q < r1;
+    const bool st = own && hf == 0 && t >= 0 && t < nrows;
     const __amdgpu_buffer_rsrc_t r = rv;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r,
                                            CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0,
@@ -1059,8 +1085,9 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   //   (a/sc) [u/k - (L u + u (g (2 x0 + t) - (3 x0 (x0 + t) + t^2)))/2],  t = a u,
   // without the cancellation of two G evaluations (and without reading G0).
   const double zs = a_alpha * isc;
-  auto centre = [&](ix_t r) {
-    const dv2 (*d)[64] = lg[(r - r0) & 1];
+  auto centre = [&](ix_t t) {
+    const ix_t r = prow(t);
+    const dv2 (*d)[64] = lg[t & 1];
     const dv2 x0r = d[NB][lane];
     dv2 wo;
 #pragma unroll
@@ -1075,7 +1102,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
       wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
     }
-    const bool in = own && r < r1;
+    const bool in = own && t < nrows;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
                                            CO((in && hf == 0) ? uint32_t(r * nx + col) * 8u : kOOB,
                                               nelem),
@@ -1098,8 +1125,8 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     avv = __builtin_fma(vh.y, vm.y, __builtin_fma(vh.x, vm.x, avv));
     aww = __builtin_fma(wh.y, wm.y, __builtin_fma(wh.x, wm.x, aww));
   };
-  auto push_h2 = [&](const Slot& s, ix_t q) {
-    const dv2 h2 = push(s, q);
+  auto push_h2 = [&](const Slot& s, ix_t t) {
+    const dv2 h2 = push(s, t);
     h2w[0] = h2w[1];
     h2w[1] = h2w[2];
     h2w[2] = h2;
@@ -1122,31 +1149,33 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const bool edge_band = A.hs_ld > 0 && (top || bot);
   if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, 0, cst, a_tau);  // uniform per block
   if (nrows > 0) {
-    // prologue: rows r0-2, r0-1 (band halo), r0, r0+1 enter the window (r0, r0+1 also the
-    // LDS lag); rows r0+2 .. r0+1+PF go in flight.  Row q >= r0+2 uses register slot
-    // (q - r0 - 2) mod RR.  At most 2 + PF rows of loads are live at once.
+    // prologue (logical rows, march order): rows -2, -1 (band halo) and 0, 1 enter the window
+    // (0, 1 also the LDS lag); rows 2 .. 1+PF go in flight.  Row t >= 2 uses register slot
+    // (t - 2) mod RR.  At most 2 + PF rows of loads are live at once.
     {
-      Slot P[2];
-      load(P[0], r0 - 2);
-      load(P[1], r0 - 1);
-      push_h2(P[0], r0 - 2);
-      push_h2(P[1], r0 - 1);
-      load(P[0], r0);
-      load(P[1], r0 + 1);
       Slot S[RR];
+      {
+        Slot P[2];
+        load(P[0], -2, TMc{});
+        load(P[1], -1, TMc{});
+        push_h2(P[0], -2);
+        push_h2(P[1], -1);
+        load(P[0], 0, TMc{});
+        load(P[1], 1, TMc{});
 #pragma unroll
-      for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
-      push_h2(P[0], r0);
-      stash(P[0], gq, r0);
-      push_h2(P[1], r0 + 1);
-      stash(P[1], gq, r0 + 1);
-      {  // halo pairs of rows r0-1 (window slot 2) and r0 (slot 3)
+        for (int d = 0; d < PF; ++d) load(S[d], 2 + d, TMc{});
+        push_h2(P[0], 0);
+        stash(P[0], gq, 0);
+        push_h2(P[1], 1);
+        stash(P[1], gq, 1);
+      }
+      {  // halo pairs of rows -1 (window slot 2) and 0 (slot 3)
         if constexpr (mb) {
           u32x4 a0, b0, a1, b1;
-          poll(r0 - 1, &a0, &b0);
-          poll(r0, &a1, &b1);
-          fixup(hw[2], h2w[0], mb_halo(r0 - 1, a0, b0));
-          fixup(hw[3], h2w[1], mb_halo(r0, a1, b1));
+          poll(-1, &a0, &b0);
+          poll(0, &a1, &b1);
+          fixup(hw[2], h2w[0], mb_halo(-1, a0, b0));
+          fixup(hw[3], h2w[1], mb_halo(0, a1, b1));
         }
       }
       // whole groups of RR rows with no branch inside the group (a branch would make the
@@ -1155,15 +1184,15 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
       for (ix_t t0 = 0; t0 < nrows; t0 += RR) {
 #pragma unroll
         for (int k = 0; k < RR; ++k) {
-          const ix_t r = r0 + t0 + k;
+          const ix_t t = t0 + k;
           u32x4 ma, mb2;
-          if constexpr (mb) poll(r + 1, &ma, &mb2);  // before the row's batch: its wait
+          if constexpr (mb) poll(t + 1, &ma, &mb2);  // before the row's batch: its wait
                                                      // leaves the batch in flight
-          load(S[(k + PF) % RR], r + 2 + PF);  // the slot of row r+1, consumed last step
-          push_h2(S[k], r + 2);
-          if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(r + 1, ma, mb2));  // row r+1
-          centre(r);
-          stash(S[k], gq, r + 2);  // into the LDS slot row r just vacated
+          load(S[(k + PF) % RR], t + 2 + PF, NTc{});  // the slot of row t+1, consumed last step
+          push_h2(S[k], t + 2);
+          if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(t + 1, ma, mb2));  // row t+1
+          centre(t);
+          stash(S[k], gq, t + 2);  // into the LDS slot row t just vacated
         }
       }
     }
@@ -1257,6 +1286,11 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const ix_t r0 = opaque_s<kPinScalars<NV>>(ix_t(A.r_begin) + band * A.RY);
   const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
   const ix_t nrows = r1 - r0;
+  const bool dn = A.alt <= 0 || (band & 1) == 1;  // march direction, as in arnoldi_kernel
+  const ix_t rb = opaque_s<kPinScalars<NV>>(dn ? r0 : r1 - 1);
+  const ix_t rs = dn ? 1 : -1;
+  using NTc = std::integral_constant<bool, NT>;
+  using TMc = std::integral_constant<bool, false>;
   const SHCoef& K = A.k;
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
@@ -1306,12 +1340,16 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const bool slab = A.yh != nullptr;
   const double* yhb = slab ? A.yh : A.x0;
   const ix_t yld = (A.yh_ld > 0) ? A.yh_ld : nx;  // row stride of the halo rows
-  auto wrap = [&](ix_t q) -> ix_t {
-    q = (q > r1 + 1) ? r1 + 1 : q;
+  auto prow = [&](ix_t t) -> ix_t {  // logical row t -> physical, as in arnoldi_kernel
+    t = (t > nrows + 1) ? nrows + 1 : t;
+    return rb + rs * t;
+  };
+  auto wrap = [&](ix_t t) -> ix_t {
+    const ix_t q = prow(t);
     return (q < 0) ? q + ny : ((q >= ny) ? q - ny : q);
   };
-  auto halo_row = [&](ix_t q) -> bool {
-    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;
+  auto halo_row = [&](ix_t t) -> bool {
+    const ix_t qc = prow(t);
     return slab && (qc < 0 || qc >= ny);
   };
 
@@ -1329,16 +1367,16 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const int pside = needL ? 0 : 1;
   const ix_t fcol = needL ? (B0 - 2 + nx) % nx : (B0 + BW) % nx;
   bool mb_dead = A.mb_recompute;
-  auto mb_need = [&](ix_t q) -> bool { return (needL || needR) && !halo_row(q); };
-  auto poll = [&](ix_t q, u32x4* a, u32x4* b) {
-    const bool on = mb_need(q) && !mb_dead;
-    const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
-    ARN_CHK(!on || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
+  auto mb_need = [&](ix_t t) -> bool { return (needL || needR) && !halo_row(t); };
+  auto poll = [&](ix_t t, u32x4* a, u32x4* b) {
+    const bool on = mb_need(t) && !mb_dead;
+    const uint32_t o = mb_off(Lnb, mbT, t + 2, nside, 0);
+    ARN_CHK(!on || (t + 2 >= 0 && t + 2 < mbT && int64_t(o) + 32 <= A.mb_cap * 8));
     *a = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o : kOOB, 0, kMBCoh);
     *b = __builtin_amdgcn_raw_buffer_load_b128(rmb, on ? o + 16 : kOOB, 0, kMBCoh);
   };
-  auto recompute = [&](ix_t q) -> dv2 {  // push()'s update sum, entry order (rolled loop)
-    const ix_t o2 = CI(wrap(q) * nx + fcol, nelem - 1);
+  auto recompute = [&](ix_t t) -> dv2 {  // push()'s update sum, entry order (rolled loop)
+    const ix_t o2 = CI(wrap(t) * nx + fcol, nelem - 1);
     dv2 v{0.0, 0.0};
 #pragma unroll 1
     for (int e = 0; e <= NV; ++e) {
@@ -1349,12 +1387,12 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
     return v;
   };
-  auto mb_halo = [&](ix_t q, u32x4 a, u32x4 b) -> dv2 {
-    const bool need = mb_need(q);
+  auto mb_halo = [&](ix_t t, u32x4 a, u32x4 b) -> dv2 {
+    const bool need = mb_need(t);
     bool ok = !need || (!mb_dead && mb_tag_ok(a, tag) && mb_tag_ok(b, tag));
     dv2 h{mb_val(a), mb_val(b)};
     if (!ok) {
-      const uint32_t o = mb_off(Lnb, mbT, q - r0 + 2, nside, 0);
+      const uint32_t o = mb_off(Lnb, mbT, t + 2, nside, 0);
       for (int n = 0; n < kMBSpin && !mb_dead && !ok; ++n) {
         __builtin_amdgcn_s_sleep(2);
         a = __builtin_amdgcn_raw_buffer_load_b128(rmb, o, 0, kMBCoh);
@@ -1365,7 +1403,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
         h = dv2{mb_val(a), mb_val(b)};
       } else {
         mb_dead = true;
-        h = recompute(q);
+        h = recompute(t);
       }
     }
     return need ? h : dv2{-0.0, -0.0};
@@ -1376,18 +1414,18 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     double hv, hx;
     bool own;
   };
-  auto load = [&](Slot& s, ix_t q) {
-    const ix_t qq = wrap(q);
+  auto load = [&](Slot& s, ix_t t, auto pol) {  // pol as in arnoldi_kernel
+    const ix_t qq = wrap(t);
     const ix_t o = CI(qq * nx + col, nelem - 1);
-    const ix_t qc = (q > r1 + 1) ? r1 + 1 : q;
-    const bool hrow = halo_row(q);
+    const ix_t qc = prow(t);
+    const bool hrow = halo_row(t);
     const ix_t hq = hrow ? ((qc < 0) ? qc + 2 : qc - ny + 2) : 0;
     const ix_t yo = CI(hq * yld + col, 4 * yld - 1);
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const double* a = src(e) + o;
       if (e == EX) a = hrow ? yhb + yo : a;
-      s.e[e] = gld2<NT>(a);
+      s.e[e] = gld2<decltype(pol)::value>(a);
     }
     const ix_t ho = CI(qq * nx + hcol, nelem);
     if constexpr (!EXT && !mb) {
@@ -1398,8 +1436,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     s.hx = gld((hrow && lane < 4) ? yhb + hyo : (mb ? A.x0 : hxp + ho));
     s.own = !hrow;
   };
-  auto stash = [&](const Slot& s, const dv2& g, ix_t q) {
-    dv2 (*d)[64] = lg[(q - r0) & 1];
+  auto stash = [&](const Slot& s, const dv2& g, ix_t t) {
+    dv2 (*d)[64] = lg[t & 1];
 #pragma unroll
     for (int e = 0; e < NV; ++e) d[e][lane] = s.e[e];
     d[NV][lane] = g;
@@ -1409,7 +1447,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
 #pragma unroll
   for (int m = 0; m < 5; ++m) yw[m] = hw[m] = vw[m] = dv2{0.0, 0.0};
   dv2 gq{0.0, 0.0};
-  auto push = [&](const Slot& s, ix_t q) {
+  auto push = [&](const Slot& s, ix_t t) {
+    const ix_t q = prow(t);
     dv2 v{0.0, 0.0};
 #pragma unroll
     for (int e = 0; e <= NV; ++e) {  // entry order (the slab edge kernel sums the same way)
@@ -1423,12 +1462,12 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
       u = s.own ? s.e[EZ] : xe;
     else
       u = s.own ? v : xe;
-    const int slot = int(q & 1);
+    const int slot = int(t & 1);
     {  // mailbox: publish u on this block's first / last column pair
       if constexpr (mb) {
         const bool pq = prod && s.own;
-        const uint32_t po = mb_off(L, mbT, q - r0 + 2, pside, 0);
-        ARN_CHK(!pq || (q - r0 + 2 >= 0 && q - r0 + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
+        const uint32_t po = mb_off(L, mbT, t + 2, pside, 0);
+        ARN_CHK(!pq || (t + 2 >= 0 && t + 2 < mbT && int64_t(po) + 32 <= A.mb_cap * 8));
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.x, tag), rmb, pq ? po : kOOB, 0, kMBCoh);
         __builtin_amdgcn_raw_buffer_store_b128(mb_rec(u.y, tag), rmb, pq ? po + 16 : kOOB, 0,
                                                kMBCoh);
@@ -1483,7 +1522,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     yw[4] = u;
     hw[4] = dv2{cm1 + u.y, u.x + cp2};
     vw[4] = v;
-    const bool st = own && q >= r0 && q < r1;
+    const bool st = own && t >= 0 && t < nrows;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rv,
                                            CO(st ? uint32_t(q * nx + col) * 8u : kOOB, nelem), 0,
                                            kOutPol);
@@ -1503,8 +1542,9 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
 #pragma unroll
   for (int m = 0; m < 3; ++m) h2w[m] = dv2{0.0, 0.0};
   const double zs = a_alpha * isc;
-  auto centre = [&](ix_t r) {  // closed-form FD quotient as in arnoldi_kernel
-    const dv2 (*d)[64] = lg[(r - r0) & 1];
+  auto centre = [&](ix_t t) {  // closed-form FD quotient as in arnoldi_kernel
+    const ix_t r = prow(t);
+    const dv2 (*d)[64] = lg[t & 1];
     const dv2 x0r = d[NV][lane];
     dv2 wo;
 #pragma unroll
@@ -1519,7 +1559,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
       const double D = K.g * (2.0 * x + t) - (3.0 * x * (x + t) + t * t);
       wo[q] = zs * (uc * K.ik - (Lu + uc * D) / 2);
     }
-    const bool in = own && r < r1;
+    const bool in = own && t < nrows;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, wo), rw,
                                            CO(in ? uint32_t(r * nx + col) * 8u : kOOB, nelem), 0, kOutPol);
     if (A.hs_ld > 0) push_edge_row(A.PS + 2, A.hs_ld, r, ny, col, in, wo);
@@ -1538,8 +1578,8 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     aw[NV + 1] = __builtin_fma(vm.y, vm.y, __builtin_fma(vm.x, vm.x, aw[NV + 1]));
     aw[NV + 2] = __builtin_fma(wm.y, wm.y, __builtin_fma(wm.x, wm.x, aw[NV + 2]));
   };
-  auto push_h2 = [&](const Slot& s, ix_t q) {
-    const dv2 h2 = push(s, q);
+  auto push_h2 = [&](const Slot& s, ix_t t) {
+    const dv2 h2 = push(s, t);
     h2w[0] = h2w[1];
     h2w[1] = h2w[2];
     h2w[2] = h2;
@@ -1555,41 +1595,43 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau, top, bot);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (top || bot);
   if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, NV + 1, cst, a_tau);
-  if (nrows > 0) {
-    Slot P[2];
-    load(P[0], r0 - 2);
-    load(P[1], r0 - 1);
-    push_h2(P[0], r0 - 2);
-    push_h2(P[1], r0 - 1);
-    load(P[0], r0);
-    load(P[1], r0 + 1);
+  if (nrows > 0) {  // logical rows, march order (see arnoldi_kernel)
     Slot S[RR];
+    {
+      Slot P[2];
+      load(P[0], -2, TMc{});
+      load(P[1], -1, TMc{});
+      push_h2(P[0], -2);
+      push_h2(P[1], -1);
+      load(P[0], 0, TMc{});
+      load(P[1], 1, TMc{});
 #pragma unroll
-    for (int d = 0; d < PF; ++d) load(S[d], r0 + 2 + d);
-    push_h2(P[0], r0);
-    stash(P[0], gq, r0);
-    push_h2(P[1], r0 + 1);
-    stash(P[1], gq, r0 + 1);
+      for (int d = 0; d < PF; ++d) load(S[d], 2 + d, TMc{});
+      push_h2(P[0], 0);
+      stash(P[0], gq, 0);
+      push_h2(P[1], 1);
+      stash(P[1], gq, 1);
+    }
     {
       if constexpr (mb) {
         u32x4 a0, b0, a1, b1;
-        poll(r0 - 1, &a0, &b0);
-        poll(r0, &a1, &b1);
-        fixup(hw[2], h2w[0], mb_halo(r0 - 1, a0, b0));
-        fixup(hw[3], h2w[1], mb_halo(r0, a1, b1));
+        poll(-1, &a0, &b0);
+        poll(0, &a1, &b1);
+        fixup(hw[2], h2w[0], mb_halo(-1, a0, b0));
+        fixup(hw[3], h2w[1], mb_halo(0, a1, b1));
       }
     }
     for (ix_t t0 = 0; t0 < nrows; t0 += RR) {  // no branch inside a group (see arnoldi_kernel)
 #pragma unroll
       for (int k = 0; k < RR; ++k) {
-        const ix_t r = r0 + t0 + k;
+        const ix_t t = t0 + k;
         u32x4 ma, mb2;
-        if constexpr (mb) poll(r + 1, &ma, &mb2);
-        load(S[(k + PF) % RR], r + 2 + PF);
-        push_h2(S[k], r + 2);
-        if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(r + 1, ma, mb2));
-        centre(r);
-        stash(S[k], gq, r + 2);
+        if constexpr (mb) poll(t + 1, &ma, &mb2);
+        load(S[(k + PF) % RR], t + 2 + PF, NTc{});
+        push_h2(S[k], t + 2);
+        if constexpr (mb) fixup(hw[3], h2w[1], mb_halo(t + 1, ma, mb2));
+        centre(t);
+        stash(S[k], gq, t + 2);
       }
     }
   }
@@ -1624,6 +1666,13 @@ int env_int(const char* name, int dflt) {
 }
 
 std::atomic<int64_t> g_mbox_launches{0};
+
+// alternating march direction by default (NKHIP_ARN_ALT=0: every band marches down; read per
+// launch, for A/B runs)
+bool arnoldi_alt_default() {
+  const char* e = std::getenv("NKHIP_ARN_ALT");
+  return !(e && e[0] == '0');
+}
 
 struct Occ {
   int ncu = 0, blocks_per_cu = 0;
@@ -1690,6 +1739,7 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& oc
   A.strips = int(strips);
   A.nbands = int(P.nbands);
   A.RY = int(P.RY);
+  if (A.alt < 0) A.alt = arnoldi_alt_default() ? 1 : 0;
   if (mbox) {
     kern = kern_mb;  // the mailbox instantiation
     g_mbox_launches.fetch_add(1, std::memory_order_relaxed);

@@ -387,3 +387,54 @@ def test_fused_kernel_mailbox_every_length(monkeypatch):
         wr = (_torch_G(x0 + sc * zs * vr, h, r, k, g) - G0) / sc
         assert float((v1 - vr).abs().max()) <= 1e-13 * float(vr.abs().max()), nv
         assert float((w1 - wr).abs().max()) <= 1e-9 * float(wr.abs().max()), nv
+
+
+@pytest.mark.parametrize("ny,nx", [(512, 4096), (64, 1024), (40, 130), (24, 600), (8, 512)])
+@pytest.mark.parametrize("nv", [1, 4, 8, 18, 19, 27, 35])
+@pytest.mark.parametrize("ext", [False, True])
+def test_fused_kernel_march_direction(ny, nx, nv, ext, monkeypatch):
+    """Alternating march (arnoldi.hip "March direction": odd bands march up their rows so that
+    adjacent bands read their shared halo rows at the same time) against every band marching
+    down (NKHIP_ARN_ALT=0, the kernel before round 6): v, w' and the edge arrays written for them
+    bitwise the same -- the stencil adds the rows either side of the centre commutatively -- and
+    the dot products, whose per-wave row order is reversed in the odd bands, within rounding.
+    512 x 4096 is the N = 8 rank's slab of the 4096^2 headline."""
+    import nkhip
+    gen = torch.Generator(device="cpu").manual_seed(nv * 13 + nx + ny + int(ext))
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    V = [rnd() for _ in range(nv)]
+    coef = [float(c) for c in torch.randn(nv, generator=gen, dtype=torch.float64)]
+    w, x0 = rnd(), rnd()
+    z = rnd() if ext else None
+    args = (V, coef, w, 0.75, x0, None, 0.625, 0.01, 0.2, 1.0, 0.5, 1e-3)
+    E = [nkhip.edge_gather(t) for t in V + [w]]
+    res = {}
+    for alt in ("0", "1"):
+        monkeypatch.setenv("NKHIP_ARN_ALT", alt)
+        Ev = torch.full_like(E[0], float("nan"))
+        Ew = torch.full_like(E[0], float("nan"))
+        v, wo, d = nkhip.sh_arnoldi_fused(*args, z=z, E=E, Ev_out=Ev, Ew_out=Ew)
+        res[alt] = (v, wo, d, Ev, Ew)
+    (v0, w0, d0, Ev0, Ew0), (v1, w1, d1, Ev1, Ew1) = res["0"], res["1"]
+    assert torch.equal(v0, v1) and torch.equal(w0, w1)
+    assert torch.equal(Ev0, Ev1) and torch.equal(Ew0, Ew1)
+    scale = float(w0.norm()) * float(max(t.norm() for t in V + [v0])) + float(v0.norm()) ** 2
+    assert max(abs(a - b) for a, b in zip(d0, d1)) <= 1e-13 * scale
+
+
+@pytest.mark.parametrize("ny,nx", [(512, 1024), (96, 130)])
+def test_march_direction_solve(ny, nx, monkeypatch):
+    """The solver with the alternating march (default) reaches the root of the all-down march
+    (NKHIP_ARN_ALT=0) to 1e-8 of the state's scale with Newton counts within one, is
+    deterministic, and its output is a root of the reference residual (sh_scipy_nk.py:47-49)."""
+    monkeypatch.setenv("NKHIP_ARN_ALT", "0")
+    U0, a, sa, _ = _step(ny, nx, fused=True)
+    monkeypatch.setenv("NKHIP_ARN_ALT", "1")
+    _, b, sb, pb = _step(ny, nx, fused=True)
+    _, c, sc_, _ = _step(ny, nx, fused=True)
+    assert np.array_equal(b, c) and sb == sc_
+    assert pb["arnoldi_fused"]["launches"] > 0
+    assert abs(sa[0]["nit"] - sb[0]["nit"]) <= 1
+    assert np.abs(a - b).max() <= 1e-8 * max(1.0, np.abs(a).max())
+    F = sh_oracle.residual(b.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
+    assert np.abs(F).max() <= 1e-9
