@@ -305,7 +305,8 @@ __device__ __forceinline__ double edge_u(const ArnoldiArgs& A, int64_t o, int h0
 // versa): a whole launch apart, so both reads come from HBM -- on short slabs 4 extra rows per
 // band are a large share (a 512-row slab: PMC traffic 1.15x of algorithmic for the pair layout's
 // 32-row bands, 1.22-1.39x for the wide layout's 8-16-row bands; profiles/r06a_slab512_kernels.txt).
-// With A.alt the even bands march UP their rows: two adjacent bands then reach their shared
+// In the ALT instantiations (taken for bands of at most 32 rows, arnoldi_alt_mode) the even
+// bands march UP their rows: two adjacent bands then reach their shared
 // boundary at the same moment -- both at their start, or both at their end.  The bands of one XCD
 // are a contiguous run starting at an even band (the blockIdx mapping below), so its boundaries
 // 2b | 2b+1 are start-start ones, and the prologue loads its rows temporally (the interior stays
@@ -692,7 +693,7 @@ __device__ __forceinline__ void arn_tail(const ArnoldiArgs& A, int64_t nblocks, 
 #endif
 }
 
-template <int NV, bool EXT, int PF, bool NT, bool MB, int WB>
+template <int NV, bool EXT, int PF, bool ALT, bool MB, int WB>
 __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
   double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
@@ -741,12 +742,13 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
   const ix_t nrows = r1 - r0;
   // march direction ("March direction" above): logical row t of the band is physical row
-  // rb + rs t -- r0 + t marching down, r1 - 1 - t marching up (odd bands under A.alt)
-  const bool dn = A.alt <= 0 || (band & 1) == 1;
+  // rb + rs t -- r0 + t marching down, r1 - 1 - t marching up (the even bands of an ALT
+  // instantiation)
+  const bool dn = !ALT || (band & 1) == 1;
   const ix_t rb = opaque_s<kPinScalars<NV>>(dn ? r0 : r1 - 1);
   const ix_t rs = dn ? 1 : -1;
-  using NTc = std::integral_constant<bool, NT>;
-  using TMc = std::integral_constant<bool, false>;
+  using NTc = std::integral_constant<bool, true>;   // the row loop: non-temporal
+  using TMc = std::integral_constant<bool, !ALT>;   // the prologue: temporal under ALT
   const SHCoef K = A.k;
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
@@ -917,10 +919,10 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     double hx;
     bool own;  // row of this slab (false: a neighbour's halo row, u taken from A.yh)
   };
-  // pol: the streamed loads' cache policy -- NTc (non-temporal where NT is set) in the row loop,
-  // TMc (temporal) in the prologue, whose rows the neighbouring band reads as well ("March
-  // direction").  A compile-time choice: a runtime select between the two load forms is merged
-  // into one plain load (the non-temporal hint dropped)
+  // pol: the streamed loads' cache policy -- NTc (non-temporal) in the row loop, TMc in the
+  // prologue (temporal in the ALT instantiation: its rows are read by the neighbouring band as
+  // well, "March direction").  A compile-time choice: a runtime select between the two load
+  // forms is merged into one plain load (the non-temporal hint dropped)
   auto load = [&](Slot& s, ix_t t, auto pol) {
     const ix_t qq = wrap(t);
     const ix_t o = CI(qq * nx + col, nelem - 1);
@@ -1249,7 +1251,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
 constexpr int kWW = 128;       // columns per wave
 constexpr int kWideMaxNV = 18;  // LDS: 2 rows x (nv + 1) x 4 waves x 1 KB <= 152 KB
 
-template <int NV, bool EXT, int PF, bool NT, int W, bool MB>
+template <int NV, bool EXT, int PF, bool ALT, int W, bool MB>
 __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs A) {
   const double a_tau = arn_tau(A), a_alpha = arn_alpha(A), a_sc = arn_sc(A);
   double cst[NV];  // update coefficients, loaded together (independent loads, one wait)
@@ -1286,11 +1288,11 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const ix_t r0 = opaque_s<kPinScalars<NV>>(ix_t(A.r_begin) + band * A.RY);
   const ix_t r1 = opaque_s<kPinScalars<NV>>((r0 + A.RY < rend) ? r0 + A.RY : rend);
   const ix_t nrows = r1 - r0;
-  const bool dn = A.alt <= 0 || (band & 1) == 1;  // march direction, as in arnoldi_kernel
+  const bool dn = !ALT || (band & 1) == 1;  // march direction, as in arnoldi_kernel
   const ix_t rb = opaque_s<kPinScalars<NV>>(dn ? r0 : r1 - 1);
   const ix_t rs = dn ? 1 : -1;
-  using NTc = std::integral_constant<bool, NT>;
-  using TMc = std::integral_constant<bool, false>;
+  using NTc = std::integral_constant<bool, true>;   // the row loop: non-temporal
+  using TMc = std::integral_constant<bool, !ALT>;   // the prologue: temporal under ALT
   const SHCoef& K = A.k;
   const double isc = 1.0 / a_sc;
   const __amdgpu_buffer_rsrc_t rv = rsrc(A.out_v, ny * nx);
@@ -1667,11 +1669,13 @@ int env_int(const char* name, int dflt) {
 
 std::atomic<int64_t> g_mbox_launches{0};
 
-// alternating march direction by default (NKHIP_ARN_ALT=0: every band marches down; read per
-// launch, for A/B runs)
-bool arnoldi_alt_default() {
+// the alternating march (the ALT instantiations) for bands of at most kAltMaxRY rows;
+// NKHIP_ARN_ALT=1 / 0 forces it on / off (read per launch, for A/B runs and tests)
+constexpr int64_t kAltMaxRY = 32;
+bool arnoldi_alt_mode(int64_t ry) {
   const char* e = std::getenv("NKHIP_ARN_ALT");
-  return !(e && e[0] == '0');
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return ry <= kAltMaxRY;
 }
 
 struct Occ {
@@ -1681,10 +1685,21 @@ struct Occ {
 // Grid of one resident round of waves (NKHIP_ARN_ROUNDS scales it) for a kernel whose blocks own
 // `nwb` waves of `cw` columns each; bands of >= 8 rows, and no more partial columns than the
 // caller's buffer holds.  `occ` = that kernel's occupancy.
+// The instantiations of one launch: the plain / mailbox kernels and their alternating-march
+// twins (ALT), with their occupancies
+template <class K>
+struct Kerns {
+  K kern, kern_mb, kern_a, kern_mb_a;
+  Occ occ, occ_mb, occ_a, occ_mb_a;
+};
+
 template <int NV, class K>
-hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& occ_mb, int nwb_mb,
-                       bool has_mb, int cw, ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
-  if (occ.ncu == 0 || occ_mb.ncu == 0) return hipErrorUnknown;
+hipError_t launch_grid(const Kerns<K>& KS, int nwb, int nwb_mb, bool has_mb, int cw,
+                       ArnoldiArgs A, hipStream_t s, int64_t* nwaves) {
+  const Occ &occ = KS.occ, &occ_mb = KS.occ_mb;
+  K kern = KS.kern, kern_mb = KS.kern_mb;
+  if (occ.ncu == 0 || occ_mb.ncu == 0 || KS.occ_a.ncu == 0 || KS.occ_mb_a.ncu == 0)
+    return hipErrorUnknown;
   static const int rounds = env_int("NKHIP_ARN_ROUNDS", 1);
   // the shortest band (NKHIP_ARN_MIN_RY, default 8 rows): short slabs trade resident waves for
   // fewer band prologues
@@ -1739,7 +1754,16 @@ hipError_t launch_grid(K kern, const Occ& occ, int nwb, K kern_mb, const Occ& oc
   A.strips = int(strips);
   A.nbands = int(P.nbands);
   A.RY = int(P.RY);
-  if (A.alt < 0) A.alt = arnoldi_alt_default() ? 1 : 0;
+  // the alternating march where bands are short (its temporal prologue costs on tall bands:
+  // profiles/r06_short_slab.md), with the same occupancy as the plan's kernel
+  const Occ& oa = mbox ? KS.occ_mb_a : KS.occ_a;
+  const Occ& op = mbox ? occ_mb : occ;
+  if (A.alt < 0) A.alt = arnoldi_alt_mode(P.RY) ? 1 : 0;
+  if (A.alt && oa.blocks_per_cu != op.blocks_per_cu) A.alt = 0;
+  if (A.alt) {
+    kern = KS.kern_a;
+    kern_mb = KS.kern_mb_a;
+  }
   if (mbox) {
     kern = kern_mb;  // the mailbox instantiation
     g_mbox_launches.fetch_add(1, std::memory_order_relaxed);
@@ -1768,42 +1792,58 @@ Occ query_occ(K kern, int threads) {
   return o;
 }
 
-template <int NV, bool EXT, int PF, bool NT>
+template <int NV, bool EXT, int PF>
 hipError_t launch_t(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   constexpr int WM = EXT ? WPB : kMbWPB;
-  auto kern = arnoldi_kernel<NV, EXT, PF, NT, false, WPB>;
-  auto kern_mb = arnoldi_kernel<NV, EXT, PF, NT, !EXT, WM>;  // EXT: no mailbox, the same kernel
   if (NV + 1 > 16 * WPB) return hipErrorInvalidValue;  // one packed halo load per row
-  static const Occ occ = query_occ(kern, 64 * WPB);
-  static const Occ occ_mb = query_occ(kern_mb, 64 * WM);
-  return launch_grid<NV>(kern, occ, WPB, kern_mb, occ_mb, WM, !EXT, kSW, A, s, nwaves);
+  using K = decltype(&arnoldi_kernel<NV, EXT, PF, false, false, WPB>);
+  // EXT: no mailbox, the same kernel
+  static const Kerns<K> KS = [] {
+    Kerns<K> k{arnoldi_kernel<NV, EXT, PF, false, false, WPB>,
+               arnoldi_kernel<NV, EXT, PF, false, !EXT, WM>,
+               arnoldi_kernel<NV, EXT, PF, true, false, WPB>,
+               arnoldi_kernel<NV, EXT, PF, true, !EXT, WM>, {}, {}, {}, {}};
+    k.occ = query_occ(k.kern, 64 * WPB);
+    k.occ_mb = query_occ(k.kern_mb, 64 * WM);
+    k.occ_a = query_occ(k.kern_a, 64 * WPB);
+    k.occ_mb_a = query_occ(k.kern_mb_a, 64 * WM);
+    return k;
+  }();
+  return launch_grid<NV>(KS, WPB, WM, !EXT, kSW, A, s, nwaves);
 }
 
 constexpr int kWideW = 4;  // waves per block of the wide layout (512 columns)
-template <int NV, bool EXT, int PF, bool NT>
+template <int NV, bool EXT, int PF>
 hipError_t launch_wide(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   // no mailbox instantiation: with 512-column blocks the packed halo is the cheaper one
   // (4096^2, one box: n4 0.63 vs 0.55, n12 0.64 vs 0.63, n18 0.62 vs 0.57 of 8 TB/s)
   // (the wide kernel keeps a mailbox instantiation parameter, MB; it measured no gain with 2- or
   // 4-wave blocks, profiles/r02_arnoldi_ab.md, and is not instantiated)
-  auto kern = arnoldi_wide_kernel<NV, EXT, PF, NT, kWideW, false>;
-  static const Occ occ = query_occ(kern, 64 * kWideW);
-  return launch_grid<NV>(kern, occ, kWideW, kern, occ, kWideW, false, kWW, A, s, nwaves);
+  using K = decltype(&arnoldi_wide_kernel<NV, EXT, PF, false, kWideW, false>);
+  static const Kerns<K> KS = [] {
+    Kerns<K> k{arnoldi_wide_kernel<NV, EXT, PF, false, kWideW, false>,
+               arnoldi_wide_kernel<NV, EXT, PF, false, kWideW, false>,
+               arnoldi_wide_kernel<NV, EXT, PF, true, kWideW, false>,
+               arnoldi_wide_kernel<NV, EXT, PF, true, kWideW, false>, {}, {}, {}, {}};
+    k.occ = k.occ_mb = query_occ(k.kern, 64 * kWideW);
+    k.occ_a = k.occ_mb_a = query_occ(k.kern_a, 64 * kWideW);
+    return k;
+  }();
+  return launch_grid<NV>(KS, kWideW, kWideW, false, kWW, A, s, nwaves);
 }
 
 template <int NV, bool EXT>
 hipError_t launch_pf(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
-  static const bool nt = env_int("NKHIP_ARN_NT", 1) != 0;
   constexpr int PF = pf_for(NV);
 #ifdef NKHIP_ARN_TUNE  // tuning build (`make tune`): NKHIP_ARN_PF selects the rows in flight
   static const int pf = env_int("NKHIP_ARN_PF", 0);
   if constexpr (NV % 4 == 0) {
     switch (pf) {
-      case 1: return launch_t<NV, EXT, 1, true>(A, s, nwaves);
-      case 2: return launch_t<NV, EXT, 2, true>(A, s, nwaves);
-      case 3: return launch_t<NV, EXT, 3, true>(A, s, nwaves);
-      case 4: return launch_t<NV, EXT, 4, true>(A, s, nwaves);
-      case 6: return launch_t<NV, EXT, 6, true>(A, s, nwaves);
+      case 1: return launch_t<NV, EXT, 1>(A, s, nwaves);
+      case 2: return launch_t<NV, EXT, 2>(A, s, nwaves);
+      case 3: return launch_t<NV, EXT, 3>(A, s, nwaves);
+      case 4: return launch_t<NV, EXT, 4>(A, s, nwaves);
+      case 6: return launch_t<NV, EXT, 6>(A, s, nwaves);
       default: break;
     }
   }
@@ -1811,11 +1851,10 @@ hipError_t launch_pf(const ArnoldiArgs& A, hipStream_t s, int64_t* nwaves) {
   if constexpr (NV <= kWideMaxNV) {
     if (arnoldi_wide(NV)) {
       constexpr int PFW = NV <= 4 ? 3 : (NV <= 10 ? 2 : 1);
-      return nt ? launch_wide<NV, EXT, PFW, true>(A, s, nwaves)
-                : launch_wide<NV, EXT, PFW, false>(A, s, nwaves);
+      return launch_wide<NV, EXT, PFW>(A, s, nwaves);
     }
   }
-  return nt ? launch_t<NV, EXT, PF, true>(A, s, nwaves) : launch_t<NV, EXT, PF, false>(A, s, nwaves);
+  return launch_t<NV, EXT, PF>(A, s, nwaves);
 }
 
 template <bool EXT, int NV = 1>

@@ -277,9 +277,10 @@ struct ArnoldiArgs {
   int64_t mb_cap = 0;  // doubles at mb
   uint64_t mb_tag = 0;
   bool mb_recompute = false;  // test switch: every halo pair takes the mailbox's recompute path
-  // alternating march (arnoldi.hip "March direction"): odd bands march up their rows, so the rows
-  // two adjacent bands both read (each one's band halo) are read by both at the same time and
-  // the second read hits the XCD's L2.  Set by arnoldi_launch (NKHIP_ARN_ALT; -1: its default).
+  // alternating march (arnoldi.hip "March direction"): the ALT instantiations, whose even bands
+  // march up their rows and load their prologue temporally, so the rows two adjacent bands both
+  // read are read at the same time and the second read hits the XCD's L2.  Set by arnoldi_launch
+  // (-1: for bands of at most 32 rows; NKHIP_ARN_ALT=1 / 0 forces it on / off).
   int alt = -1;
   ArnTail tail{};             // reduction + control in the launch's last blocks (S: on)
 };

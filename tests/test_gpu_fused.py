@@ -438,3 +438,27 @@ def test_march_direction_solve(ny, nx, monkeypatch):
     assert np.abs(a - b).max() <= 1e-8 * max(1.0, np.abs(a).max())
     F = sh_oracle.residual(b.reshape(-1), U0.reshape(-1), ny, nx, 0.625, 0.01, 0.2, 1.0)
     assert np.abs(F).max() <= 1e-9
+
+
+@pytest.mark.parametrize("ny,nx,nv,alt", [(512, 4096, 24, "1"), (512, 4096, 8, "1"),
+                                          (4096, 4096, 8, "0"), (4096, 4096, 24, "0")])
+def test_march_direction_auto(ny, nx, nv, alt, monkeypatch):
+    """Without NKHIP_ARN_ALT the host takes the alternating march for bands of at most 32 rows
+    (arnoldi.hip arnoldi_alt_mode): the N = 8 rank's 512-row slab (pair layout: 32-row bands,
+    wide: 16) runs it, the 4096-row grid (64- and 256-row bands) does not.  The dot products of
+    the two marches differ in rounding, so bitwise equality of every output names the path."""
+    import nkhip
+    gen = torch.Generator(device="cpu").manual_seed(nv + ny)
+    rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
+    V = [rnd() for _ in range(nv)]
+    coef = [float(c) for c in torch.randn(nv, generator=gen, dtype=torch.float64)]
+    w, x0 = rnd(), rnd()
+    args = (V, coef, w, 0.75, x0, None, 0.625, 0.01, 0.2, 1.0, 0.5, 1e-3)
+    monkeypatch.delenv("NKHIP_ARN_ALT", raising=False)
+    v, wo, d = nkhip.sh_arnoldi_fused(*args)
+    monkeypatch.setenv("NKHIP_ARN_ALT", alt)
+    v1, w1, d1 = nkhip.sh_arnoldi_fused(*args)
+    monkeypatch.setenv("NKHIP_ARN_ALT", "1" if alt == "0" else "0")
+    v2, w2, d2 = nkhip.sh_arnoldi_fused(*args)
+    assert torch.equal(v, v1) and torch.equal(wo, w1) and d == d1
+    assert torch.equal(v, v2) and torch.equal(wo, w2) and d != d2  # the other march: dots only
