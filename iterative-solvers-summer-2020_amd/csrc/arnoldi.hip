@@ -396,16 +396,25 @@ __device__ __forceinline__ void slab_x_exchange(const ArnoldiArgs& A, int64_t ba
 // march as with exchanged halo rows.  No exchange runs between the control and this launch, and
 // no block waits for another rank.  (A halo column shared with the neighbouring block is written
 // by both with the same bits.)
-template <int NV>
+// items per thread for one round over `items` points with `lanes` threads, capped by the values
+// it holds: every basis length up to 34 fits 5 x NE beside the march; nv 35's kernel sits at the
+// 512-register ceiling and spills already at 4 (20 B scratch), so it keeps round 5's 2
+constexpr int push_kmax(int NV, int items, int lanes) {
+  const int k = (items + lanes - 1) / lanes, cap = (NV >= 35) ? 2 : 175 / (NV + 1);
+  return k < cap ? k : (cap > 0 ? cap : 1);
+}
+
+template <int NV, int KMAX>
 __device__ __forceinline__ void slab_push_prologue(const ArnoldiArgs& A, bool first, bool last, int64_t B0,
                                    int64_t BW, int h0, const double* cst, double a_tau) {
   const int64_t nx = A.nx, ld = A.hs_ld;
   double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
   constexpr int NE = NV + 1;
-  // (row, column) items per thread and round: each round's loads are in flight together (one
-  // memory latency); 2 x NE values stay below the march's register peak, so the prologue does
-  // not raise the kernel's register count (and with it lower its occupancy)
-  constexpr int KMAX = 2;
+  // KMAX (row, column) items per thread and round: each round's loads are in flight together
+  // (one latency of the fine-grained slot memory), and the caller's KMAX covers a block's
+  // 2 (BW + 4) items in ONE round (round 6: 2 per thread left the +4 halo columns to a second
+  // round, a third for the wide layout's 512-column blocks) while KMAX x NE values stay below the
+  // march's register peak (push_kmax)
   const int64_t ncol = BW + 4;  // columns B0-2 .. B0+BW+1 of the two halo rows
   const int64_t nb = blockDim.x, items = 2 * ncol;
   for (int side = 0; side < 2; ++side) {
@@ -459,14 +468,15 @@ __device__ __forceinline__ void slab_push_prologue(const ArnoldiArgs& A, bool fi
 
 // v (or w') of own row q into the neighbours' halo slots when q is one of the slab's edge rows
 // (ps[0]: the previous rank's slot, rows 2, 3 <- rows 0, 1; ps[1]: the next rank's, rows 0, 1 <-
-// rows ny-2, ny-1); `st`: this lane stores row q (wave-uniform row, per-lane column)
+// rows ny-2, ny-1); `st`: this lane stores row q (wave-uniform row, per-lane column); written
+// through to the slot (store_sys16), drained at the band's end
 __device__ __forceinline__ void push_edge_row(double* const* ps, int64_t ld, int64_t q,
                                               int64_t ny, int64_t col, bool st, dv2 val) {
   const bool top = q < 2, bot = q >= ny - 2;
   if (!(st && (top || bot))) return;
   double* d = top ? ps[0] + (2 + q) * ld : ps[1] + (q - (ny - 2)) * ld;
   ARN_CHK(col + 1 < ld);
-  *reinterpret_cast<dv2*>(d + col) = val;
+  store_sys16(d + col, val.x, val.y);
 }
 
 // 32-bit row / column indices of the pair kernel's row loop, and a uniform value the compiler
@@ -1149,7 +1159,10 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const bool top = r0 < 2, bot = r1 + 2 > ny;
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau, top, bot);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (top || bot);
-  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, 0, cst, a_tau);  // uniform per block
+  // (one round of slot loads for the block's 2 (BW + 4) halo-row points)
+  if (edge_band)
+    slab_push_prologue<NV, push_kmax(NV, 2 * (BW + 4), 64 * WB)>(A, top, bot, B0, BW, 0, cst,
+                                                                a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue (logical rows, march order): rows -2, -1 (band halo) and 0, 1 enter the window
     // (0, 1 also the LDS lag); rows 2 .. 1+PF go in flight.  Row t >= 2 uses register slot
@@ -1200,7 +1213,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
   }
 
-  if (edge_band) __threadfence_system();  // the pushed edge rows, before the kernel ends
+  if (edge_band) drain_pushes();  // the pushed edge rows (push_edge_row), before the kernel ends
   // one partial per wave: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']; entry 2k + hf of
   // load k is summed over its half (width-32 butterflies)
 #pragma unroll
@@ -1596,7 +1609,9 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const bool top = r0 < 2, bot = r1 + 2 > ny;  // as in arnoldi_kernel
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau, top, bot);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (top || bot);
-  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, NV + 1, cst, a_tau);
+  if (edge_band)
+    slab_push_prologue<NV, push_kmax(NV, 2 * (BW + 4), 64 * W)>(A, top, bot, B0, BW, NV + 1, cst,
+                                                                     a_tau);
   if (nrows > 0) {  // logical rows, march order (see arnoldi_kernel)
     Slot S[RR];
     {
@@ -1638,7 +1653,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
   }
 
-  if (edge_band) __threadfence_system();  // the pushed edge rows, before the kernel ends
+  if (edge_band) drain_pushes();  // the pushed edge rows (push_edge_row), before the kernel ends
   wave_sum<NV + 3>(aw);
   wave_sum<NV>(ag);
   if (lane == 0) {

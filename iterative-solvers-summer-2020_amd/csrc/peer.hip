@@ -96,7 +96,8 @@ __global__ void __launch_bounds__(kHaloBlock) peer_halo_kernel(const PeerArgs a,
 }
 
 // Pushed halo rows (arnoldi.hip): v's rows 0, 1 -> rows 2, 3 of the previous rank's slot, rows
-// ny-2, ny-1 -> rows 0, 1 of the next rank's slot, then a system-scope fence.  Nothing waits.
+// ny-2, ny-1 -> rows 0, 1 of the next rank's slot, written through (store_sys8) and drained.
+// Nothing waits.
 __global__ void __launch_bounds__(kHaloBlock) push_rows_kernel(const double* v, double* pp,
                                                               double* pn, int64_t ny, int64_t nx,
                                                               int64_t ld) {
@@ -105,8 +106,8 @@ __global__ void __launch_bounds__(kHaloBlock) push_rows_kernel(const double* v, 
   double* dst = (t < 2) ? pp + (2 + t) * ld : pn + (t - 2) * ld;
   const int64_t step = int64_t(gridDim.x) * kHaloBlock;
   for (int64_t j = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x; j < nx; j += step)
-    dst[j] = v[row * nx + j];
-  __threadfence_system();
+    store_sys8(dst + j, v[row * nx + j]);
+  drain_pushes();
 }
 
 // what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)

@@ -16,6 +16,7 @@
 
 #include "nk_device.h"
 #include "nk_kernels.h"
+#include "peer_dev.h"
 
 namespace nk {
 
@@ -270,13 +271,14 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
   for (int k = 0; k < NR - 1; ++k) combine(k);
 
   double red[3] = {0.0, 0.0, 0.0};
-  bool pushed = false;  // this thread wrote rows into a neighbour's halo slot (fence at the end)
-  // a pushed edge row (global slab row g of e_ny) of an output into the neighbours' slots
+  bool pushed = false;  // this thread wrote rows into a neighbour's halo slot (drained at the end)
+  // a pushed edge row (global slab row g of e_ny) of an output into the neighbours' slots,
+  // written through (store_sys16)
   auto push_row = [&](double* const* ps, int64_t g, double2 v) {
     const bool top = g < 2, bot = g >= A.e_ny - 2;
     if (!(top || bot)) return;
     double* d = top ? ps[0] + (2 + g) * A.ps_ld : ps[1] + (g - (A.e_ny - 2)) * A.ps_ld;
-    *reinterpret_cast<double2*>(d + cc) = v;
+    store_sys16(d + cc, v.x, v.y);
     pushed = true;
   };
   for (int64_t base = 0; base < nrows; base += RING) {
@@ -355,7 +357,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
       }
     }
   }
-  if (pushed) __threadfence_system();  // the pushed rows, before the pass ends
+  if (pushed) drain_pushes();  // the pushed rows, before the pass ends
   if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
     const int64_t nblk = int64_t(gx) * gy;
