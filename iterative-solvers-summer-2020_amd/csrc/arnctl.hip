@@ -44,6 +44,28 @@ __device__ void upload_state(ArnCtlState* S, const ArnCtlState* H, int rows) {
   __threadfence();  // the state before the control reads it (this wave, another lane's stores)
 }
 
+// The hand-off from the reducing blocks to the last one without fences (arnoldi.hip "Tail", the
+// same form): every value stored sc1 and drained, one agent-scope counter add per block, the last
+// block's wave loads the values sc1 into LDS.  (An agent-scope __threadfence per block wrote
+// back and invalidated its XCD's L2 and the system fence of the one-GPU kernel did the same,
+// behind every fused launch.)  true: this block arrived last.
+__device__ __forceinline__ bool reduced_arrive(ArnCtlState* S) {
+  drain_stores();
+  return __hip_atomic_fetch_add(&S->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+         gridDim.x - 1;
+}
+// the last block's first wave: the n values into LDS (vals), the counter reset for the next
+// launch (stream order)
+__device__ __forceinline__ void reduced_collect(ArnCtlState* S, const double* result, double* vals,
+                                                int n) {
+  const int lane = int(threadIdx.x);
+  for (int i = lane; i < n; i += 64) vals[i] = ld_sc1(result + i);
+  if (lane == 0) __hip_atomic_store(&S->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __global__ void __launch_bounds__(64) arn_ctl_kernel(ArnCtlState* S, ArnCtlState* H,
                                                      const double* red, double* red_host,
                                                      double* prm, uint32_t* status, int t, int up) {
@@ -59,18 +81,18 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
   const int k = blockIdx.x;
   const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, true);
   __shared__ bool last;
+  __shared__ double vals[kRedMax];  // the last block's copy of every block's value
   if (threadIdx.x == 0) {
-    result[k] = s;
-    if (result_host) result_host[k] = s;
-    __threadfence_system();  // this block's result before its arrival (the host reads it too)
-    last = atomicAdd(&S->arrive, 1u) == gridDim.x - 1;
+    // written through and drained before counting in (reduced_arrive)
+    st_sc1(result + k, s);
+    if (result_host) result_host[k] = s;  // pinned host memory: not cached
+    last = reduced_arrive(S);
   }
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
-  __threadfence();  // every other block's result is visible after its arrival
-  if (threadIdx.x == 0) S->arrive = 0;  // for the next launch (stream order)
+  reduced_collect(S, result, vals, int(gridDim.x));
   __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  ctl_body(S, H, result, nullptr, prm, status, t, G);
+  ctl_body(S, H, vals, nullptr, prm, status, t, G);
 }
 
 // Row slabs over the peer-memory communicator: the reduction, the all-reduce of its nval sums
@@ -85,22 +107,25 @@ __global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
   const int k = blockIdx.x;
   const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, true);
   __shared__ bool last;
+  __shared__ double vals[kRedMax];  // the last block's copy of every block's value
   if (threadIdx.x == 0) {
-    result[k] = s;
-    __threadfence();
-    last = atomicAdd(&S->arrive, 1u) == gridDim.x - 1;
+    st_sc1(result + k, s);
+    last = reduced_arrive(S);
   }
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
-  __threadfence();
-  if (threadIdx.x == 0) S->arrive = 0;
-  if (!peer_allreduce_wave(pa, result, int(gridDim.x), int(gridDim.x))) {
+  const int n = int(gridDim.x);
+  reduced_collect(S, result, vals, n);
+  if (!peer_allreduce_wave(pa, vals, n, n)) {
     if (threadIdx.x == 0) prm[kArnMaxNV + 3] = 1.0;  // the queued fused step does nothing
     return;
   }
-  __threadfence();  // the combined values (other lanes' stores) before the control reads them
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // the combined values in LDS
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  for (int i = int(threadIdx.x); i < n; i += 64) result[i] = vals[i];
   __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  ctl_body(S, H, result, result_host, prm, status, t, G);
+  ctl_body(S, H, vals, result_host, prm, status, t, G);
 }
 
 }  // namespace
@@ -117,7 +142,8 @@ hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, dou
 hipError_t arn_reduce_ctl_launch(const double* partial, int64_t nblk, int nval, double* result,
                                  double* result_host, ArnCtlState* S, ArnCtlState* H, double* prm,
                                  uint32_t* status, int t, hipStream_t s) {
-  if (!partial || !result || !S || !H || !prm || !status || nval < 1 || t < 0 || t > kMaxVec)
+  if (!partial || !result || !S || !H || !prm || !status || nval < 1 || nval > kRedMax || t < 0 ||
+      t > kMaxVec)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(arn_reduce_ctl_kernel, dim3(unsigned(nval)), dim3(RB), 0, s, partial, nblk,
                      result, result_host, S, H, prm, status, t);

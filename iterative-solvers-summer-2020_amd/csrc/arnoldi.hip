@@ -396,25 +396,18 @@ __device__ __forceinline__ void slab_x_exchange(const ArnoldiArgs& A, int64_t ba
 // march as with exchanged halo rows.  No exchange runs between the control and this launch, and
 // no block waits for another rank.  (A halo column shared with the neighbouring block is written
 // by both with the same bits.)
-// items per thread for one round over `items` points with `lanes` threads, capped by the values
-// it holds: every basis length up to 34 fits 5 x NE beside the march; nv 35's kernel sits at the
-// 512-register ceiling and spills already at 4 (20 B scratch), so it keeps round 5's 2
-constexpr int push_kmax(int NV, int items, int lanes) {
-  const int k = (items + lanes - 1) / lanes, cap = (NV >= 35) ? 2 : 175 / (NV + 1);
-  return k < cap ? k : (cap > 0 ? cap : 1);
-}
-
-template <int NV, int KMAX>
+template <int NV>
 __device__ __forceinline__ void slab_push_prologue(const ArnoldiArgs& A, bool first, bool last, int64_t B0,
                                    int64_t BW, int h0, const double* cst, double a_tau) {
   const int64_t nx = A.nx, ld = A.hs_ld;
   double* yh = const_cast<double*>(A.yh);  // 4 rows of nx (yh_ld == nx), this launch's scratch
   constexpr int NE = NV + 1;
-  // KMAX (row, column) items per thread and round: each round's loads are in flight together
-  // (one latency of the fine-grained slot memory), and the caller's KMAX covers a block's
-  // 2 (BW + 4) items in ONE round (round 6: 2 per thread left the +4 halo columns to a second
-  // round, a third for the wide layout's 512-column blocks) while KMAX x NE values stay below the
-  // march's register peak (push_kmax)
+  // (row, column) items per thread and round: each round's loads are in flight together (one
+  // memory latency); 2 x NE values stay below the march's register peak, so the prologue does
+  // not raise the kernel's register count (and with it lower its occupancy).  (Round 6: one
+  // round for all of a block's 2 (BW + 4) items measured no faster, and the larger prologue
+  // tipped the compiler into wrong code for the wide EXT kernels, profiles/r06_short_slab.md 8)
+  constexpr int KMAX = 2;
   const int64_t ncol = BW + 4;  // columns B0-2 .. B0+BW+1 of the two halo rows
   const int64_t nb = blockDim.x, items = 2 * ncol;
   for (int side = 0; side < 2; ++side) {
@@ -530,22 +523,7 @@ constexpr bool kPinScalars = NV <= 33;
 // ArnTail::wait_ticks (device_wait_ticks, from the wall-clock rate); device_steps resets the
 // arrival counters before every run of device steps, so a launch that gave up leaves no count
 // behind for the next run.
-// Write-through (sc1) 8-B stores and loads: the hand-off between the blocks of one launch with
-// no release fence (MI355X_MICROARCH.md "Valid forms", first row: every byte stored sc1, every
-// storing wave drained, one agent-scope counter add per block; every load of the bytes sc1).
-// An agent-scope fence per block would write back its XCD's whole L2 (the launch's freshly
-// written output vectors) and invalidate its L1 under the blocks still streaming.
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                     static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double(static_cast<long long>(
-      __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
-                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-}
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// (st_sc1 / ld_sc1 / drain_stores: nk_device.h)
 
 #ifdef ARN_TAIL_PROBE  // timing build (scripts/dbg/tail_probe.py): stage times of the tails
 __device__ unsigned long long g_tail_probe[8];  // [0] tails, [1..5] summed stage ticks
@@ -1159,10 +1137,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
   const bool top = r0 < 2, bot = r1 + 2 > ny;
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, 0, a_tau, top, bot);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (top || bot);
-  // (one round of slot loads for the block's 2 (BW + 4) halo-row points)
-  if (edge_band)
-    slab_push_prologue<NV, push_kmax(NV, 2 * (BW + 4), 64 * WB)>(A, top, bot, B0, BW, 0, cst,
-                                                                a_tau);  // uniform per block
+  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, 0, cst, a_tau);  // uniform per block
   if (nrows > 0) {
     // prologue (logical rows, march order): rows -2, -1 (band halo) and 0, 1 enter the window
     // (0, 1 also the LDS lag); rows 2 .. 1+PF go in flight.  Row t >= 2 uses register slot
@@ -1213,7 +1188,7 @@ __global__ void __launch_bounds__(64 * WB) arnoldi_kernel(const ArnoldiArgs A) {
     }
   }
 
-  if (edge_band) drain_pushes();  // the pushed edge rows (push_edge_row), before the kernel ends
+  if (edge_band) drain_stores();  // the pushed edge rows (push_edge_row), before the kernel ends
   // one partial per wave: [w'.V_i (nv)] [w'.v] [v.V_i (nv)] [v.v] [w'.w']; entry 2k + hf of
   // load k is summed over its half (width-32 butterflies)
 #pragma unroll
@@ -1609,9 +1584,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
   const bool top = r0 < 2, bot = r1 + 2 > ny;  // as in arnoldi_kernel
   if (A.x.me) slab_x_exchange<NV>(A, band, B0, BW, NV + 1, a_tau, top, bot);  // uniform per block
   const bool edge_band = A.hs_ld > 0 && (top || bot);
-  if (edge_band)
-    slab_push_prologue<NV, push_kmax(NV, 2 * (BW + 4), 64 * W)>(A, top, bot, B0, BW, NV + 1, cst,
-                                                                     a_tau);
+  if (edge_band) slab_push_prologue<NV>(A, top, bot, B0, BW, NV + 1, cst, a_tau);
   if (nrows > 0) {  // logical rows, march order (see arnoldi_kernel)
     Slot S[RR];
     {
@@ -1653,7 +1626,7 @@ __global__ void __launch_bounds__(64 * W) arnoldi_wide_kernel(const ArnoldiArgs 
     }
   }
 
-  if (edge_band) drain_pushes();  // the pushed edge rows (push_edge_row), before the kernel ends
+  if (edge_band) drain_stores();  // the pushed edge rows (push_edge_row), before the kernel ends
   wave_sum<NV + 3>(aw);
   wave_sum<NV>(ag);
   if (lane == 0) {

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(kHaloBlock) push_rows_kernel(const double* v, 
   const int64_t step = int64_t(gridDim.x) * kHaloBlock;
   for (int64_t j = int64_t(blockIdx.x) * kHaloBlock + threadIdx.x; j < nx; j += step)
     store_sys8(dst + j, v[row * nx + j]);
-  drain_pushes();
+  drain_stores();
 }
 
 // what a rank publishes about its buffer (nk_comm_peer_handle_bytes bytes)

@@ -52,24 +52,22 @@ __host__ __device__ inline int64_t buffer_bytes(int P, int64_t max_nx) {
 
 // A store into a peer's halo slot (pushed halo rows): 16 B with the system-scope policy bits, so
 // it is written through this XCD's L2 to the slot's memory and the producer only drains its own
-// stores (s_waitcnt) before it ends -- no system fence, whose L2 write-back + invalidate of the
+// stores (drain_stores) before it ends -- no system fence, whose L2 write-back + invalidate of the
 // whole XCD cost the fused Arnoldi launch's edge bands ~6 us at its end (round 6,
 // profiles/r06_short_slab.md section 7).  The s_nop is the wait state a store of more than 8 B
 // needs before its data registers are rewritten, which the compiler's hazard check does not see
 // through an asm statement.  (One 16-B store rather than two 8-B atomic stores: the latter cost
 // the nv-35 Arnoldi kernel, at the register ceiling, a 20-B scratch spill.)
-__device__ __forceinline__ void store_sys16(double* d, double a, double b) {
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  const d2v v2 = {a, b};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 0" ::"v"(d), "v"(v2) : "memory");
-}
 __device__ __forceinline__ void store_sys8(double* d, double a) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(d),
                      static_cast<unsigned long long>(__double_as_longlong(a)), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// this wave's stores acknowledged (the pushes above: in the slot's memory)
-__device__ __forceinline__ void drain_pushes() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void store_sys16(double* d, double a, double b) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const d2v v2 = {a, b};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 0" ::"v"(d), "v"(v2) : "memory");
+}
 
 struct PeerArgs {
   char* base[kMaxPeers];  // every rank's buffer in this address space (mine: base[rank])

@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(BX) march_kernel(StencilArgs A, int RY, int gx
       }
     }
   }
-  if (pushed) drain_pushes();  // the pushed rows, before the pass ends
+  if (pushed) drain_stores();  // the pushed rows, before the pass ends
   if constexpr (kRed<M>) {
     const double v = block_reduce<3, 1, BX>(red);
     const int64_t nblk = int64_t(gx) * gy;

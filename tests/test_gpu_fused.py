@@ -92,6 +92,22 @@ def _torch_G(y, h, r, k, g):
 @pytest.mark.parametrize("nv", [1, 5, 18, 35])
 @pytest.mark.parametrize("ext", [False, True])
 def test_fused_kernel_vs_torch(ny, nx, nv, ext):
+    _check_fused_vs_torch(ny, nx, nv, ext)
+
+
+@pytest.mark.parametrize("ny,nx", [(40, 130), (24, 600)])
+@pytest.mark.parametrize("nv", list(range(1, 36)))
+@pytest.mark.parametrize("ext", [False, True])
+def test_fused_kernel_every_basis_length(ny, nx, nv, ext):
+    """Every instantiation of the fused kernel (each basis length has its own, in both layouts'
+    ranges, with and without z) against the torch reference, on short bands (the alternating
+    march) and ragged widths.  A round-6 build that passed the solver tests computed w' wrong at
+    wave boundaries in the nv-7 wide kernel with z only (the compiler's output for that one
+    instantiation, profiles/r06_short_slab.md section 8): no instantiation is trusted untested."""
+    _check_fused_vs_torch(ny, nx, nv, ext)
+
+
+def _check_fused_vs_torch(ny, nx, nv, ext):
     import nkhip
     gen = torch.Generator(device="cpu").manual_seed(nv * 100 + nx)
     rnd = lambda: torch.randn(ny, nx, generator=gen, dtype=torch.float64).cuda()  # noqa: E731
