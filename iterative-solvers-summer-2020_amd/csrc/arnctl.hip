@@ -22,6 +22,17 @@ namespace {
 
 constexpr int RB = 1024;  // reduction block (as reduce_final_kernel)
 
+#ifdef ARN_CTL_PROBE  // timing build (scripts/dbg/ctl_probe.py): stage times of the control launch
+// [0] launches, [1] first block's entry -> last block counted in, [2] -> values collected,
+// [3] -> all-reduced, [4] -> control done, [5] first entry -> last block's entry
+__device__ unsigned long long g_ctl_probe[8];
+__device__ unsigned long long g_ctl_t0 = ~0ull;   // this launch's first entry (reset by the last)
+__device__ unsigned long long g_ctl_tl = 0;       // this launch's last entry
+#define CTL_STAMP(v) const unsigned long long v = wall_clock64()
+#else
+#define CTL_STAMP(v)
+#endif
+
 // up > 0: first copy the host's pinned loop state H to S (the fields before R, and the Gram rows
 // 0 .. up-2) -- the entry of a run of device steps, which would otherwise take two runtime blits
 // (H is mapped device-visible memory).  All loads are issued before the first store.
@@ -78,6 +89,10 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
                                                             double* result, double* result_host,
                                                             ArnCtlState* S, ArnCtlState* H,
                                                             double* prm, uint32_t* status, int t) {
+  // the control's loads (first wave of every block), in flight during the reduction (they
+  // lengthen it by ~1 us, but issued after it they cost more: profiles/r06_short_slab.md 9)
+  CtlPre P;
+  if (threadIdx.x < 64) ctl_load(S, t, P);
   const int k = blockIdx.x;
   const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, true);
   __shared__ bool last;
@@ -91,8 +106,7 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
   reduced_collect(S, result, vals, int(gridDim.x));
-  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  ctl_body(S, H, vals, nullptr, prm, status, t, G);
+  ctl_run(S, H, vals, nullptr, prm, status, t, P);
 }
 
 // Row slabs over the peer-memory communicator: the reduction, the all-reduce of its nval sums
@@ -104,6 +118,17 @@ __global__ void __launch_bounds__(RB) arn_reduce_ctl_kernel(const double* partia
 __global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
     const double* partial, int64_t nblk, double* result, double* result_host, const PeerArgs pa,
     ArnCtlState* S, ArnCtlState* H, double* prm, uint32_t* status, int t) {
+#ifdef ARN_CTL_PROBE
+  if (threadIdx.x == 0) {
+    const unsigned long long e = wall_clock64();
+    atomicMin(&g_ctl_t0, e);
+    atomicMax(&g_ctl_tl, e);
+  }
+#endif
+  // the control's loads (first wave of every block), in flight during the reduction (they
+  // lengthen it by ~1 us, but issued after it they cost more: profiles/r06_short_slab.md 9)
+  CtlPre P;
+  if (threadIdx.x < 64) ctl_load(S, t, P);
   const int k = blockIdx.x;
   const double s = reduce_column<RB>(partial + int64_t(k) * nblk, nblk, true);
   __shared__ bool last;
@@ -114,21 +139,47 @@ __global__ void __launch_bounds__(RB) arn_reduce_allreduce_ctl_kernel(
   }
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
+  CTL_STAMP(p_last);
   const int n = int(gridDim.x);
   reduced_collect(S, result, vals, n);
-  if (!peer_allreduce_wave(pa, vals, n, n)) {
+  CTL_STAMP(p_coll);
+  if (!peer_allreduce_wave_wt(pa, vals, n, n)) {
     if (threadIdx.x == 0) prm[kArnMaxNV + 3] = 1.0;  // the queued fused step does nothing
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // the combined values in LDS
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  CTL_STAMP(p_ar);
   for (int i = int(threadIdx.x); i < n; i += 64) result[i] = vals[i];
-  __shared__ double G[kArnMaxNV + 1][kArnMaxNV + 1];
-  ctl_body(S, H, vals, result_host, prm, status, t, G);
+  ctl_run(S, H, vals, result_host, prm, status, t, P);
+#ifdef ARN_CTL_PROBE
+  CTL_STAMP(p_end);
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = atomicAdd(&g_ctl_t0, 0ull), tl = atomicAdd(&g_ctl_tl, 0ull);
+    atomicAdd(&g_ctl_probe[0], 1ull);
+    atomicAdd(&g_ctl_probe[1], p_last - t0);
+    atomicAdd(&g_ctl_probe[2], p_coll - p_last);
+    atomicAdd(&g_ctl_probe[3], p_ar - p_coll);
+    atomicAdd(&g_ctl_probe[4], p_end - p_ar);
+    atomicAdd(&g_ctl_probe[5], tl - t0);
+    atomicExch(&g_ctl_t0, ~0ull);
+    atomicExch(&g_ctl_tl, 0ull);
+  }
+#endif
 }
 
 }  // namespace
+
+#ifdef ARN_CTL_PROBE
+extern "C" int nk_debug_ctl_probe(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ctl_probe), sizeof(g_ctl_probe)) != hipSuccess)
+    return -1;
+  static const unsigned long long zero[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ctl_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t arn_ctl_launch(ArnCtlState* S, ArnCtlState* H, const double* red, double* red_host,
                           double* prm, uint32_t* status, int t, hipStream_t s, int upload_rows) {

@@ -107,13 +107,16 @@ __device__ __forceinline__ uint64_t* xflag(char* b, int P, int64_t max_nx, int p
 // the interior bands stream).  The bound is elapsed time on the constant-rate wall clock
 // (`ticks` of wall_clock64(), set from hipDeviceAttributeWallClockRate on the host), checked
 // every 64 polls, so it holds whatever one poll costs.
+// ACQ false: no acquire after the tag (the caller reads the published data with system-scope
+// loads, which go past the caches anyway)
+template <bool ACQ = true>
 __device__ inline bool wait_flag_tag(const uint64_t* flag, uint64_t tag, const char* me, int* err,
                                      uint64_t ticks) {
   const uint64_t* abort_word = reinterpret_cast<const uint64_t*>(me + kOffAbort);
   const uint64_t t0 = wall_clock64();  // once: a wrapping poll count must not restart it
   for (uint32_t n = 0;; ++n) {
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag) {
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope
+      if constexpr (ACQ) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope
       return true;
     }
     if ((n & 63) == 0) {
@@ -199,6 +202,45 @@ __device__ inline bool peer_allreduce_wave(const PeerArgs& a, double* v, int nsu
     double acc = red_slot(mine, a.P, par, 0)[t];
     for (int q = 1; q < a.P; ++q) {
       const double x = red_slot(mine, a.P, par, q)[t];
+      acc = (t < nsum) ? acc + x : nmax(acc, x);
+    }
+    v[t] = acc;
+  }
+  return true;
+}
+
+// peer_allreduce_wave without fences (the control launches, arnctl.hip; the fused launch's tail
+// keeps the fenced form, its code being part of every fused kernel): the contributions are
+// written through to every rank's slot (store_sys8) and drained before the flags go out, the
+// flags are polled without an acquire, and the slots are read with system-scope loads.  The two
+// system fences of the fenced form write back and invalidate this XCD's L2 each.
+__device__ inline bool peer_allreduce_wave_wt(const PeerArgs& a, double* v, int nsum, int nv) {
+  const int lane = threadIdx.x & 63;
+  const int par = int(a.tag & 1);
+  for (int t = lane; t < nv; t += 64) {
+    const double x = v[t];
+    for (int q = 0; q < a.P; ++q) store_sys8(red_slot(a.base[q], a.P, par, a.rank) + t, x);
+  }
+  drain_stores();
+  __builtin_amdgcn_wave_barrier();
+  for (int q = lane; q < a.P; q += 64)
+    __hip_atomic_store(red_flag(a.base[q], par, a.rank), a.tag, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = true;
+  for (int q = lane; q < a.P; q += 64)
+    ok = ok && wait_flag_tag<false>(red_flag(a.base[a.rank], par, q), a.tag, a.base[a.rank], a.err,
+                                    a.wait_ticks);
+  if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
+  char* mine = a.base[a.rank];
+  auto ld = [](const double* p) {
+    return __longlong_as_double(static_cast<long long>(
+        __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+  };
+  for (int t = lane; t < nv; t += 64) {
+    double acc = ld(red_slot(mine, a.P, par, 0) + t);
+    for (int q = 1; q < a.P; ++q) {
+      const double x = ld(red_slot(mine, a.P, par, q) + t);
       acc = (t < nsum) ? acc + x : nmax(acc, x);
     }
     v[t] = acc;
