@@ -7,7 +7,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-O=gpurun_out/r06g_chain.log
+O=gpurun_out/${1:-r06g}_chain.log
 for rep in 1 2; do
   for v in host devctl tail; do
     case $v in
