@@ -386,7 +386,8 @@ __device__ __forceinline__ void slab_x_exchange(const ArnoldiArgs& A, int64_t ba
 // [V_0 .. V_{nv-1}, w] (or z) of that row -- entries the neighbours produced in EARLIER launches.
 // So every producer of an entry writes the entry's own edge rows into its ring neighbours' halo
 // slots as a by-product (this kernel for its outputs v and w', the stencil passes and
-// combinations through push_rows_launch), with a system-scope fence and no flag: the all-reduce
+// combinations through push_rows_launch), written through to the slot (store_sys16, peer_dev.h)
+// and drained by the producer, with no fence and no flag: the all-reduce
 // that every rank passes between producing an entry and the next fused launch (the device
 // control's, or the host path's) orders the writes before this launch on every rank, and a slot
 // is rewritten only when its pool vector gets new content, steps after its last reader (the same

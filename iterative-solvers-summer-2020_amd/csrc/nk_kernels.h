@@ -92,8 +92,9 @@ struct StencilArgs {
   const double* Eb = nullptr;
   int64_t e_ny = 0, e_row0 = 0;
   // pushed halo rows (peer-memory slabs, arnoldi.hip): out0's / out2's rows 0, 1 and e_ny-2,
-  // e_ny-1 also go into the previous / next rank's halo slot ([0] / [1], row stride ps_ld), with
-  // a system-scope fence -- what push_rows_launch would do after the pass
+  // e_ny-1 also go into the previous / next rank's halo slot ([0] / [1], row stride ps_ld),
+  // written through and drained (peer_dev.h store_sys16) -- what push_rows_launch would do after
+  // the pass
   double* PS0[2] = {};
   double* PS2[2] = {};
   int64_t ps_ld = 0;
@@ -314,7 +315,8 @@ int arnoldi_check_counters(int64_t* violations, int32_t* first_line, bool reset)
 int arnoldi_mailbox_counters(int64_t out[4], bool reset);
 // Pushed halo rows (peer.hip): v's rows 0, 1 -> rows 2, 3 of prev_slot and rows ny-2, ny-1 ->
 // rows 0, 1 of next_slot (the ring neighbours' halo slots of v's pool vector, row stride ld,
-// peer memory), then a system-scope fence; nothing waits (the next all-reduce orders it).
+// peer memory), written through and drained (no fence); nothing waits (the next all-reduce
+// orders it).
 hipError_t push_rows_launch(const double* v, double* prev_slot, double* next_slot, int64_t ny,
                             int64_t nx, int64_t ld, hipStream_t s);
 
